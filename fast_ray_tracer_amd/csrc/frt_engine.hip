@@ -1,0 +1,835 @@
+// frt-mi355x render engine: wavefront kernels + the C ABI of include/frt_device.h.
+//
+// The reference's per-sample recursion color_at -> shade_hit -> {lights,
+// reflected_color, refracted_color} (renderer.c:348-827) is unrolled into
+// depth levels. For one batch of camera samples:
+//
+//   k_primary  (level 0)  camera ray -> closest hit -> prepare_computations,
+//                         spawn reflection / refraction rays into queue 1
+//   k_extend   (level d)  queued ray -> closest hit -> prepare, spawn into d+1
+//   k_shadow   (level d)  one lane per (hit, light sample): ordered any-hit
+//                         walk; unshadowed counts reduced per wave, one
+//                         integer atomic per (hit, light) segment
+//   k_shade    (level d)  lighting_microfacet over the light's point row
+//   k_combine  (d = D..0) bottom-up: surface + reflected*refl + refracted*Tf*d
+//                         with the reference's schlick / dissolve order,
+//                         written into the parent's fixed child slot
+//   k_resolve             per pixel: ordered sum over (v,u) samples, /total,
+//                         (A+D+S)/3
+//
+// Children write into fixed parent slots and shadow counts are integers, so
+// the image is independent of wave scheduling. Zero-weight secondary rays
+// (refraction through opaque surfaces, Tf = 0: 94-100 % of the reference's
+// secondary rays) are not traced; their contribution is an exact 0.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "frt_device.h"
+#include "frt_shade.hpp"
+
+namespace frt {
+
+constexpr int kBlock = 256;
+
+// path-node record of one level; node i of level d belongs to queued ray i
+struct NodeRec {
+    double over_point[3];
+    double normalv[3];
+    double eyev[3];
+    double Ka[3], Kd[3], Ks[3];
+    double refl[3];
+    double Ns, over_d, rf;
+    uint64_t key;     // (global sample << 12) | heap code of the path node
+    int32_t material; // -1: the ray missed
+    int32_t parent;   // node index in level d-1 (-1 at level 0)
+    int32_t slot;     // 0 = reflected child, 1 = refracted child
+    int32_t flags;    // bit0 reflect applies, bit1 refract applies, bit2 schlick mix, bit3 dissolve
+};
+
+struct QueuedRay {
+    double o[3];
+    double d[3];
+    uint64_t key;
+    int32_t parent;
+    int32_t slot;
+};
+
+enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8 };
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31;
+    return x;
+}
+
+// area-light cache row for (path node, light, draw): the reference draws
+// rand() % cache_len twice per (hit, light) (light.c:196, renderer.c:915);
+// with a single-row cache both are row 0, as in the reference
+__device__ __forceinline__ int light_row(const frt_light& L, uint64_t seed, uint64_t key, int light, int draw) {
+    if (L.rows <= 1) return 0;
+    uint64_t h = mix64(seed ^ mix64(key * 0x9e3779b97f4a7c15ULL + (uint64_t)(light * 2 + draw + 1)));
+    return (int)(h % (uint64_t)L.rows);
+}
+
+struct Batch {
+    int64_t sample_begin;  // first global sample index of the batch
+    int64_t pixel_begin;   // first pixel (in render order) of the batch
+    int64_t num_samples;
+    int64_t row_begin, row_stride;
+    uint64_t seed;
+    int32_t spp, level;
+    int32_t remaining;     // path_length - level
+};
+
+__device__ __forceinline__ void ray_for_pixel(const frt_camera& cam, double px, double py, const double* jit, Ray& r) {
+    // renderer.c:95-129 (point aperture: the lens offset is exactly 0)
+    double xoff = (px + jit[0]) * cam.pixel_size;
+    double yoff = (py + jit[1]) * cam.pixel_size;
+    double wx = cam.half_width - xoff, wy = cam.half_height - yoff;
+    double p[3] = {wx, wy, -cam.canvas_distance}, pixel[3], origin[3];
+    xf_point(cam.inv, p, pixel);
+    double q[3] = {0.0 * cam.aperture_size, 0.0 * cam.aperture_size, 0.0};
+    xf_point(cam.inv, q, origin);
+    double v[3] = {pixel[0] - origin[0], pixel[1] - origin[1], pixel[2] - origin[2]};
+    r.o[0] = origin[0];
+    r.o[1] = origin[1];
+    r.o[2] = origin[2];
+    normalize3(v, r.d);
+}
+
+// shared tail of k_primary / k_extend: prepare, record, spawn children
+__device__ void shade_prepare(const DevScene& S, const Batch& B, const Ray& r, const Hit& h, int64_t node,
+                              uint64_t key, int32_t parent, int32_t slot, NodeRec* __restrict__ rec,
+                              QueuedRay* __restrict__ next_q, int64_t next_cap, unsigned long long* next_count,
+                              unsigned long long* counters, unsigned* err) {
+    Comps c;
+    prepare(S, r, h, c);
+    const frt_material& M = S.materials[c.material];
+    NodeRec nr;
+    for (int k = 0; k < 3; ++k) {
+        nr.over_point[k] = c.over_point[k];
+        nr.normalv[k] = c.normalv[k];
+        nr.eyev[k] = c.eyev[k];
+        nr.Ka[k] = c.Ka[k];
+        nr.Kd[k] = c.Kd[k];
+        nr.Ks[k] = c.Ks[k];
+        nr.refl[k] = c.refl[k];
+    }
+    nr.Ns = c.Ns;
+    nr.over_d = c.over_d;
+    nr.rf = 0.0;
+    nr.key = key;
+    nr.material = c.material;
+    nr.parent = parent;
+    nr.slot = slot;
+    int32_t flags = 0;
+    if (S.cfg.include_specular) {
+        const bool reflect_applies = B.remaining > 0 && M.reflective;
+        bool refract_applies = false;
+        double refr_dir[3] = {0, 0, 0};
+        if (B.remaining > 0 && c.over_d > 0.0) {  // refracted_color (renderer.c:535-573)
+            double n_ratio = c.n1 / c.n2;
+            double cos_i = dot3(c.eyev, c.normalv);
+            double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
+            if (!(sin2_t > 1.0)) {
+                refract_applies = true;
+                double cos_t = sqrt(1.0 - sin2_t);
+                double s1 = n_ratio * cos_i - cos_t;
+                for (int k = 0; k < 3; ++k) {
+                    double t1 = c.normalv[k] * s1;
+                    double t2 = c.eyev[k] * n_ratio;
+                    refr_dir[k] = t1 - t2;
+                }
+            }
+        }
+        if (reflect_applies) flags |= kReflApplies;
+        if (refract_applies) flags |= kRefrApplies;
+        if (M.reflective && c.over_d < 1.0) {
+            flags |= kMix;
+            nr.rf = schlick(c.eyev, c.normalv, c.n1, c.n2);
+        }
+        if (M.Tr > 0.0 && c.over_d > 0.0) flags |= kDissolve;
+
+        const uint64_t code = key & 0xFFFull;
+        const uint64_t base = key & ~0xFFFull;
+        // spawn only children whose weight can be non-zero (zero-weight subtrees add exactly 0)
+        if (reflect_applies && (c.refl[0] != 0.0 || c.refl[1] != 0.0 || c.refl[2] != 0.0)) {
+            unsigned long long at = atomicAdd(next_count, 1ull);
+            if ((int64_t)at < next_cap) {
+                QueuedRay q;
+                for (int k = 0; k < 3; ++k) {
+                    q.o[k] = c.over_point[k];
+                    q.d[k] = c.reflectv[k];
+                }
+                q.key = base | ((code * 2) & 0xFFFull);
+                q.parent = (int32_t)node;
+                q.slot = 0;
+                next_q[at] = q;
+            } else {
+                atomicOr(err, kErrQueueOverflow);
+            }
+        } else if (reflect_applies) {
+            atomicAdd(counters, 1ull);
+        }
+        const bool tf_zero = M.Tf[0] == 0.0 && M.Tf[1] == 0.0 && M.Tf[2] == 0.0;
+        if (refract_applies && !tf_zero) {
+            unsigned long long at = atomicAdd(next_count, 1ull);
+            if ((int64_t)at < next_cap) {
+                QueuedRay q;
+                for (int k = 0; k < 3; ++k) {
+                    q.o[k] = c.under_point[k];
+                    q.d[k] = refr_dir[k];
+                }
+                q.key = base | ((code * 2 + 1) & 0xFFFull);
+                q.parent = (int32_t)node;
+                q.slot = 1;
+                next_q[at] = q;
+            } else {
+                atomicOr(err, kErrQueueOverflow);
+            }
+        } else if (refract_applies) {
+            atomicAdd(counters, 1ull);
+        }
+    }
+    nr.flags = flags;
+    rec[node] = nr;
+}
+
+__global__ void __launch_bounds__(kBlock) k_primary(DevScene S, Batch B, NodeRec* __restrict__ rec,
+                                                    QueuedRay* __restrict__ next_q, int64_t next_cap,
+                                                    unsigned long long* next_count, unsigned long long* counters,
+                                                    unsigned* err) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B.num_samples) return;
+    const int64_t pix = B.pixel_begin + s / B.spp;
+    const int sub = (int)(s % B.spp);
+    const int64_t hs = S.cam.hsize;
+    const int64_t row = B.row_begin + (pix / hs) * B.row_stride;
+    const int64_t col = pix % hs;
+    const double* jit = S.sample_table + 2 * sub;  // sub = v * usteps + u (get_point_2d layout)
+    Ray r;
+    ray_for_pixel(S.cam, (double)col, (double)row, jit, r);
+    unsigned e = 0;
+    Hit h;
+    const uint64_t global_sample = (uint64_t)((row * hs + col) * B.spp + sub);
+    const uint64_t key = (global_sample << 12) | 1ull;
+    if (closest_hit(S, r, h, e)) {
+        shade_prepare(S, B, r, h, s, key, -1, 0, rec, next_q, next_cap, next_count, counters, err);
+    } else {
+        rec[s].material = -1;
+        rec[s].parent = -1;
+    }
+    if (e) atomicOr(err, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
+                                                   NodeRec* __restrict__ rec, QueuedRay* __restrict__ next_q,
+                                                   int64_t next_cap, unsigned long long* next_count,
+                                                   unsigned long long* counters, unsigned* err) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const QueuedRay qr = q[i];
+    Ray r;
+    for (int k = 0; k < 3; ++k) {
+        r.o[k] = qr.o[k];
+        r.d[k] = qr.d[k];
+    }
+    unsigned e = 0;
+    Hit h;
+    if (closest_hit(S, r, h, e)) {
+        shade_prepare(S, B, r, h, i, qr.key, qr.parent, qr.slot, rec, next_q, next_cap, next_count, counters, err);
+    } else {
+        NodeRec m;
+        m.material = -1;
+        m.parent = qr.parent;
+        m.slot = qr.slot;
+        rec[i].material = m.material;
+        rec[i].parent = m.parent;
+        rec[i].slot = m.slot;
+    }
+    if (e) atomicOr(err, e);
+}
+
+// one lane per (node, light sample j); lanes of a node are consecutive
+__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
+                                                   const int32_t* __restrict__ j_light,
+                                                   const int32_t* __restrict__ j_point, int32_t samples_per_node,
+                                                   int32_t* __restrict__ counts, unsigned* err) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = tid < n * samples_per_node;
+    int64_t node = 0;
+    int light = 0;
+    bool lit = false;
+    if (valid) {
+        node = tid / samples_per_node;
+        const int j = (int)(tid % samples_per_node);
+        light = j_light[j];
+        const int pt = j_point[j];
+        const NodeRec* nr = rec + node;
+        if (nr->material >= 0) {
+            const frt_light& L = S.lights[light];
+            const int row = light_row(L, B.seed, nr->key, light, 0);
+            const double* lp = S.light_points + L.points + 3 * ((int64_t)row * L.num_samples + pt);
+            // is_shadowed (renderer.c:74-93)
+            double v[3] = {lp[0] - nr->over_point[0], lp[1] - nr->over_point[1], lp[2] - nr->over_point[2]};
+            double distance = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+            Ray r;
+            r.o[0] = nr->over_point[0];
+            r.o[1] = nr->over_point[1];
+            r.o[2] = nr->over_point[2];
+            normalize3(v, r.d);
+            unsigned e = 0;
+            lit = !shadowed(S, r, distance, e);
+            if (e) atomicOr(err, e);
+        }
+    }
+    // segmented wave reduction: lanes with the same (node, light) are contiguous
+    const int lane = threadIdx.x & 63;
+    const int64_t key = valid ? node * S.num_lights + light : -1 - (int64_t)lane;
+    const int64_t prev = __shfl_up(key, 1, 64);
+    const bool head = lane == 0 || prev != key;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long lits = __ballot(lit);
+    if (valid && head) {
+        const unsigned long long above = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
+        const int next = above ? __ffsll((long long)above) - 1 : 64;
+        const unsigned long long seg = (next >= 64 ? ~0ull : ((1ull << next) - 1)) & ~((1ull << lane) - 1);
+        const int c = __popcll(lits & seg);
+        if (c) atomicAdd(counts + key, c);
+    }
+}
+
+// lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725)
+__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
+                                                  const int32_t* __restrict__ counts, double* __restrict__ surface) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeRec& nr = rec[i];
+    if (nr.material < 0) return;
+    double sA[3] = {0, 0, 0}, sD[3] = {0, 0, 0}, sS[3] = {0, 0, 0};
+    if (S.cfg.include_direct) {
+        for (int li = 0; li < S.num_lights; ++li) {
+            const frt_light& L = S.lights[li];
+            double inten;
+            if (L.type == FRT_AREA_LIGHT || L.type == FRT_CIRCLE_LIGHT) {
+                inten = (double)counts[i * S.num_lights + li] / (double)L.num_samples;  // light.c:229-242
+            } else {
+                inten = counts[i * S.num_lights + li] ? 1.0 : 0.0;  // light.c:245-251
+            }
+            double amb[3], cA[3] = {0, 0, 0}, cD[3] = {0, 0, 0}, cS[3] = {0, 0, 0};
+            for (int k = 0; k < 3; ++k) amb[k] = nr.Ka[k] * L.intensity[k];
+            if (!feq(inten, 0.0)) {
+                if (S.cfg.include_diffuse || S.cfg.include_spec_highlight) {
+                    const int row = light_row(L, B.seed, nr.key, li, 1);
+                    const double* pts = S.light_points + L.points + 3 * (int64_t)row * L.num_samples;
+                    double ned = 0.0;
+                    if (S.cfg.include_spec_highlight) ned = dot3(nr.normalv, nr.eyev);
+                    double dacc[3] = {0, 0, 0}, sacc[3] = {0, 0, 0};
+                    for (int p = 0; p < L.num_samples; ++p) {
+                        const double* lp = pts + 3 * p;
+                        double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
+                        double lv[3];
+                        normalize3(diff, lv);
+                        double ldn = dot3(lv, nr.normalv);
+                        if (S.cfg.include_diffuse && ldn >= 0.0) {
+                            for (int k = 0; k < 3; ++k) {
+                                double cc = nr.Kd[k] * L.intensity[k];
+                                cc *= ldn;
+                                dacc[k] += cc;
+                            }
+                        }
+                        if (S.cfg.include_spec_highlight && ldn >= 0.0) {
+                            double ndl = dot3(nr.normalv, lv);
+                            double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
+                            normalize3(tmp, hv);
+                            double ndh = fmax(0.0, dot3(nr.normalv, hv));
+                            double edh_inv = 1.0 / fmax(0.0, dot3(nr.eyev, hv));
+                            double ldh = dot3(lv, hv);
+                            double dist_term = (nr.Ns + 2) * pow(ndh, nr.Ns) * 0.5 * k1Pi;
+                            double gc = 2.0 * ndh * edh_inv;
+                            double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
+                            double factor = pow(1.0 - ldh, 5.0);
+                            double brdf = dist_term * geo / (4.0 * ndl * ned);
+                            for (int k = 0; k < 3; ++k) {
+                                double f = nr.Ks[k] + (1.0 - nr.Ks[k]) * factor;
+                                sacc[k] += f * L.intensity[k] * brdf;
+                            }
+                        }
+                    }
+                    double scaling = inten / (double)L.num_samples;
+                    for (int k = 0; k < 3; ++k) {
+                        cD[k] = (0.0 + dacc[k]) * scaling;
+                        cS[k] = (0.0 + sacc[k]) * scaling;
+                    }
+                }
+            }
+            if (S.cfg.include_ambient)
+                for (int k = 0; k < 3; ++k) cA[k] = 0.0 + amb[k];
+            for (int k = 0; k < 3; ++k) {
+                sA[k] += cA[k];
+                sD[k] += cD[k];
+                sS[k] += cS[k];
+            }
+        }
+    }
+    double* out = surface + 12 * i;
+    for (int k = 0; k < 3; ++k) {
+        out[k] = sA[k];
+        out[4 + k] = sD[k];
+        out[8 + k] = sS[k];
+    }
+    out[3] = out[7] = out[11] = 0.0;
+}
+
+// bottom-up combine of one level (shade_hit's specular block, renderer.c:773-822)
+__global__ void __launch_bounds__(kBlock) k_combine(const NodeRec* __restrict__ rec, int64_t n,
+                                                    const double* __restrict__ surface,
+                                                    const double* __restrict__ child,
+                                                    double* __restrict__ parent_child, double* __restrict__ sample_out,
+                                                    const frt_material* __restrict__ mats, int32_t include_specular) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeRec& nr = rec[i];
+    double col[12];
+    if (nr.material < 0) {
+        for (int k = 0; k < 12; ++k) col[k] = 0.0;
+    } else {
+        const double* s = surface + 12 * i;
+        for (int k = 0; k < 12; ++k) col[k] = s[k];
+        if (include_specular) {
+            const frt_material& M = mats[nr.material];
+            const double* R = child + 24 * i;
+            const double* T = R + 12;
+            double rl[12], rr[12];
+            for (int t = 0; t < 12; t += 4) {
+                for (int k = 0; k < 3; ++k) {
+                    rl[t + k] = (nr.flags & kReflApplies) ? 0.0 + R[t + k] * nr.refl[k] : 0.0;
+                    double tt = T[t + k] * M.Tf[k];
+                    tt *= nr.over_d;
+                    rr[t + k] = (nr.flags & kRefrApplies) ? 0.0 + tt : 0.0;
+                }
+            }
+            if (nr.flags & kMix) {
+                for (int t = 0; t < 12; t += 4) {
+                    for (int k = 0; k < 3; ++k) {
+                        rl[t + k] *= nr.rf;
+                        rr[t + k] *= 1.0 - nr.rf;
+                    }
+                }
+            }
+            for (int t = 0; t < 12; t += 4)
+                for (int k = 0; k < 3; ++k) col[t + k] += rl[t + k];
+            if (nr.flags & kDissolve)
+                for (int t = 0; t < 12; t += 4)
+                    for (int k = 0; k < 3; ++k) col[t + k] *= 1.0 - nr.over_d;
+            for (int t = 0; t < 12; t += 4)
+                for (int k = 0; k < 3; ++k) col[t + k] += rr[t + k];
+        }
+    }
+    double* dst = nr.parent >= 0 ? parent_child + 24 * (int64_t)nr.parent + 12 * nr.slot : sample_out + 12 * i;
+    if (nr.parent >= 0 && nr.material < 0) return;  // a missed child leaves its zeroed slot
+    for (int k = 0; k < 12; ++k) dst[k] = col[k];
+}
+
+// pixel_multi_sample + render_multi_helper's (A+D+S)/3 (renderer.c:132-181, 216-233)
+__global__ void __launch_bounds__(kBlock) k_resolve(const double* __restrict__ sample_col, int64_t npix, int32_t spp,
+                                                    double* __restrict__ out) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    double acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const double* s = sample_col + 12 * p * spp;
+    for (int k = 0; k < spp; ++k)
+        for (int c = 0; c < 12; ++c) acc[c] += s[12 * k + c];
+    const double total = (double)spp;
+    for (int c = 0; c < 12; ++c) acc[c] *= 1.0 / total;
+    double* o = out + 4 * p;
+    for (int k = 0; k < 3; ++k) {
+        double v = 0.0 + acc[k];
+        v += acc[4 + k];
+        v += acc[8 + k];
+        v *= 1.0 / 3.0;
+        o[k] = v;
+    }
+    o[3] = 0.0;
+}
+
+}  // namespace frt
+
+// ======================================================================
+// host side: scene upload, buffer management, frame driver, C ABI
+// ======================================================================
+
+struct frt_scene_handle {
+    int device = 0;
+    frt::DevScene S{};
+    std::vector<void*> owned;
+    hipStream_t stream = nullptr;
+    // light-sample lookup for k_shadow
+    int32_t* j_light = nullptr;
+    int32_t* j_point = nullptr;
+    int32_t samples_per_node = 0;
+    // work buffers (grow on demand)
+    struct Level {
+        frt::NodeRec* rec = nullptr;
+        frt::QueuedRay* q = nullptr;
+        double* surface = nullptr;
+        double* child = nullptr;
+        int32_t* counts = nullptr;
+        int64_t cap = 0;
+    };
+    std::vector<Level> levels;
+    double* sample_col = nullptr;
+    int64_t sample_cap = 0;
+    double* out_dev = nullptr;
+    int64_t out_cap = 0;
+    unsigned long long* counters = nullptr;  // [0..15] queue counts per level, [16] pruned
+    unsigned* err = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+
+static thread_local std::string g_last_error;
+
+static inline void hip_ignore(hipError_t) {}
+
+static int fail(const std::string& msg) {
+    g_last_error = msg;
+    return -1;
+}
+
+#define FRT_HIP(call)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (call);                                                                         \
+        if (e_ != hipSuccess) return fail(std::string(#call) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+template <typename T>
+static const T* upload(frt_scene_handle* h, const T* src, size_t count, int& rc) {
+    if (count == 0 || src == nullptr) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e != hipSuccess) {
+        rc |= fail(std::string("hipMalloc: ") + hipGetErrorString(e));
+        return nullptr;
+    }
+    h->owned.push_back(p);
+    e = hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        rc |= fail(std::string("hipMemcpy: ") + hipGetErrorString(e));
+        return nullptr;
+    }
+    return (const T*)p;
+}
+
+template <typename T>
+static int grow(T** p, int64_t& cap, int64_t need) {
+    if (need <= cap) return 0;
+    int64_t nc = std::max<int64_t>(need, cap * 2);
+    if (*p) FRT_HIP(hipFree(*p));
+    *p = nullptr;
+    FRT_HIP(hipMalloc((void**)p, (size_t)nc * sizeof(T)));
+    cap = nc;
+    return 0;
+}
+
+extern "C" {
+
+int frt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* frt_last_error(void) { return g_last_error.c_str(); }
+
+int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
+    if (sc == nullptr || out == nullptr) return fail("frt_scene_upload: null argument");
+    if (sc->abi_version != FRT_ABI_VERSION) return fail("frt_scene_upload: ABI version mismatch");
+    int ndev = frt_device_count();
+    if (ndev <= 0) return fail("frt_scene_upload: no HIP device visible");
+    if (device < 0 || device >= ndev) return fail("frt_scene_upload: device index out of range");
+    if (sc->camera.aperture_type != 6 /* POINT_APERTURE */ && sc->camera.aperture_size != 0.0)
+        return fail("frt_scene_upload: thin-lens apertures are not supported yet");
+    if (sc->camera.jitter) return fail("frt_scene_upload: jittered camera sampling is not supported yet");
+    if (!sc->config.all_ni_one) return fail("frt_scene_upload: refractive indices != 1 are not supported yet");
+    FRT_HIP(hipSetDevice(device));
+    frt_scene_handle* h = new frt_scene_handle();
+    h->device = device;
+    frt::DevScene& S = h->S;
+    int rc = 0;
+    S.nodes = upload(h, sc->nodes, (size_t)sc->num_nodes, rc);
+    S.roots = upload(h, sc->roots, (size_t)sc->num_roots, rc);
+    S.xforms = upload(h, sc->xforms, (size_t)sc->num_xforms * 16, rc);
+    S.prim = upload(h, sc->prim_data, (size_t)sc->prim_len, rc);
+    S.materials = upload(h, sc->materials, (size_t)sc->num_materials, rc);
+    S.patterns = upload(h, sc->patterns, (size_t)sc->num_patterns, rc);
+    S.textures = upload(h, sc->textures, (size_t)sc->num_textures, rc);
+    S.texels = upload(h, sc->texels, (size_t)sc->texel_len, rc);
+    S.lights = upload(h, sc->lights, (size_t)sc->num_lights, rc);
+    S.light_points = upload(h, sc->light_points, (size_t)sc->light_point_len, rc);
+    S.sample_table = upload(h, sc->sample_table, (size_t)(2 * sc->camera.usteps * sc->camera.vsteps), rc);
+    if (rc) {
+        frt_scene_release(h);
+        return -1;
+    }
+    S.num_nodes = sc->num_nodes;
+    S.num_roots = sc->num_roots;
+    S.num_lights = sc->num_lights;
+    S.num_patterns = sc->num_patterns;
+    S.cam = sc->camera;
+    S.cfg = sc->config;
+
+    std::vector<int32_t> jl, jp;
+    for (int l = 0; l < sc->num_lights; ++l)
+        for (int p = 0; p < sc->lights[l].num_samples; ++p) {
+            jl.push_back(l);
+            jp.push_back(p);
+        }
+    h->samples_per_node = (int32_t)jl.size();
+    if (!jl.empty()) {
+        h->j_light = (int32_t*)upload(h, jl.data(), jl.size(), rc);
+        h->j_point = (int32_t*)upload(h, jp.data(), jp.size(), rc);
+        if (rc) {
+            frt_scene_release(h);
+            return -1;
+        }
+    }
+    if (hipStreamCreate(&h->stream) != hipSuccess || hipMalloc((void**)&h->counters, 32 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&h->err, sizeof(unsigned)) != hipSuccess || hipEventCreate(&h->ev[0]) != hipSuccess ||
+        hipEventCreate(&h->ev[1]) != hipSuccess) {
+        frt_scene_release(h);
+        return fail("frt_scene_upload: stream / counter allocation failed");
+    }
+    h->levels.resize((size_t)std::max(1, sc->config.path_length + 2));
+    *out = h;
+    return 0;
+}
+
+void frt_scene_release(frt_scene_handle* h) {
+    if (!h) return;
+    hip_ignore(hipSetDevice(h->device));
+    for (void* p : h->owned) hip_ignore(hipFree(p));
+    for (auto& L : h->levels) {
+        hip_ignore(hipFree(L.rec));
+        hip_ignore(hipFree(L.q));
+        hip_ignore(hipFree(L.surface));
+        hip_ignore(hipFree(L.child));
+        hip_ignore(hipFree(L.counts));
+    }
+    hip_ignore(hipFree(h->sample_col));
+    hip_ignore(hipFree(h->out_dev));
+    hip_ignore(hipFree(h->counters));
+    hip_ignore(hipFree(h->err));
+    if (h->ev[0]) hip_ignore(hipEventDestroy(h->ev[0]));
+    if (h->ev[1]) hip_ignore(hipEventDestroy(h->ev[1]));
+    if (h->stream) hip_ignore(hipStreamDestroy(h->stream));
+    delete h;
+}
+
+static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
+    auto& L = h->levels[d];
+    if (need <= L.cap) return 0;
+    int64_t nc = std::max<int64_t>(need, L.cap * 2);
+    hip_ignore(hipFree(L.rec));
+    hip_ignore(hipFree(L.q));
+    hip_ignore(hipFree(L.surface));
+    hip_ignore(hipFree(L.child));
+    hip_ignore(hipFree(L.counts));
+    L.rec = nullptr;
+    L.q = nullptr;
+    L.surface = nullptr;
+    L.child = nullptr;
+    L.counts = nullptr;
+    FRT_HIP(hipMalloc((void**)&L.rec, nc * sizeof(frt::NodeRec)));
+    FRT_HIP(hipMalloc((void**)&L.q, nc * sizeof(frt::QueuedRay)));
+    FRT_HIP(hipMalloc((void**)&L.surface, nc * 12 * sizeof(double)));
+    FRT_HIP(hipMalloc((void**)&L.child, nc * 24 * sizeof(double)));
+    FRT_HIP(hipMalloc((void**)&L.counts, nc * std::max(1, h->S.num_lights) * sizeof(int32_t)));
+    L.cap = nc;
+    return 0;
+}
+
+static inline unsigned grid_for(int64_t n) { return (unsigned)((n + frt::kBlock - 1) / frt::kBlock); }
+
+struct KTimer {
+    frt_scene_handle* h;
+    frt_frame_stats* st;
+    int slot;
+    hipEvent_t a = nullptr, b = nullptr;
+    KTimer(frt_scene_handle* h_, frt_frame_stats* st_, int slot_) : h(h_), st(st_), slot(slot_) {
+        if (st) {
+            (void)hipEventCreate(&a);
+            (void)hipEventCreate(&b);
+            (void)hipEventRecord(a, h->stream);
+        }
+    }
+    ~KTimer() {
+        if (st) {
+            (void)hipEventRecord(b, h->stream);
+            (void)hipEventSynchronize(b);
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, a, b);
+            st->kernel_ms[slot] += ms;
+            st->kernel_launches[slot] += 1;
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+        }
+    }
+};
+
+static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
+    using namespace frt;
+    FRT_HIP(hipSetDevice(h->device));
+    const int64_t hs = h->S.cam.hsize;
+    const int64_t stride = P->row_stride > 0 ? P->row_stride : 1;
+    int64_t nrows = 0;
+    for (int64_t r = P->row_begin; r < P->row_end; r += stride) nrows++;
+    const int64_t npix = nrows * hs;
+    const int32_t spp = (int32_t)(h->S.cam.usteps * h->S.cam.vsteps);
+    if (spp <= 0) return fail("render: usteps*vsteps must be positive");
+    int64_t batch = P->batch_samples > 0 ? P->batch_samples : (int64_t)1 << 21;
+    int64_t pix_per_batch = std::max<int64_t>(1, batch / spp);
+    const int path = h->S.cfg.path_length;
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        (void)hipEventRecord(h->ev[0], h->stream);
+    }
+    FRT_HIP(hipMemsetAsync(h->err, 0, sizeof(unsigned), h->stream));
+    FRT_HIP(hipMemsetAsync(h->counters, 0, 32 * sizeof(unsigned long long), h->stream));
+    unsigned long long host_counters[32];
+    for (int64_t p0 = 0; p0 < npix; p0 += pix_per_batch) {
+        const int64_t bp = std::min<int64_t>(pix_per_batch, npix - p0);
+        const int64_t ns = bp * spp;
+        if (grow(&h->sample_col, h->sample_cap, ns * 12)) return -1;
+        if (ensure_level(h, 0, ns)) return -1;
+        Batch B;
+        B.sample_begin = 0;
+        // global sample index of the first sample: pixel (row, col) in frame coordinates
+        const int64_t first_row = P->row_begin + (p0 / hs) * stride;
+        B.sample_begin = (first_row * hs + p0 % hs) * spp;
+        B.pixel_begin = p0;
+        B.num_samples = ns;
+        B.row_begin = P->row_begin;
+        B.row_stride = stride;
+        B.seed = P->seed;
+        B.spp = spp;
+        std::vector<int64_t> count(path + 2, 0);
+        count[0] = ns;
+        FRT_HIP(hipMemsetAsync(h->counters, 0, 16 * sizeof(unsigned long long), h->stream));
+        for (int d = 0; d <= path; ++d) {
+            const int64_t n = count[d];
+            if (n == 0) break;
+            B.level = d;
+            B.remaining = path - d;
+            auto& L = h->levels[d];
+            if (ensure_level(h, d + 1, std::max<int64_t>(2 * n, 1024))) return -1;
+            auto& N = h->levels[d + 1];
+            FRT_HIP(hipMemsetAsync(L.child, 0, (size_t)n * 24 * sizeof(double), h->stream));
+            FRT_HIP(hipMemsetAsync(L.counts, 0, (size_t)n * std::max(1, h->S.num_lights) * sizeof(int32_t), h->stream));
+            {
+                KTimer t(h, st, d == 0 ? 5 : 0);
+                if (d == 0) {
+                    hipLaunchKernelGGL(k_primary, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, N.q,
+                                       N.cap, h->counters + d + 1, h->counters + 16, h->err);
+                } else {
+                    hipLaunchKernelGGL(k_extend, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.q, n, L.rec,
+                                       N.q, N.cap, h->counters + d + 1, h->counters + 16, h->err);
+                }
+                FRT_HIP(hipGetLastError());
+            }
+            if (h->S.cfg.include_direct && h->samples_per_node > 0) {
+                KTimer t(h, st, 1);
+                const int64_t work = n * h->samples_per_node;
+                hipLaunchKernelGGL(k_shadow, dim3(grid_for(work)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
+                                   h->j_light, h->j_point, h->samples_per_node, L.counts, h->err);
+                FRT_HIP(hipGetLastError());
+            }
+            {
+                KTimer t(h, st, 2);
+                hipLaunchKernelGGL(k_shade, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n, L.counts,
+                                   L.surface);
+                FRT_HIP(hipGetLastError());
+            }
+            FRT_HIP(hipMemcpyAsync(host_counters, h->counters, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   h->stream));
+            FRT_HIP(hipStreamSynchronize(h->stream));
+            int64_t next = (int64_t)host_counters[d + 1];
+            if (next > N.cap) {
+                unsigned e = kErrQueueOverflow;
+                FRT_HIP(hipMemcpyAsync(h->err, &e, sizeof(unsigned), hipMemcpyHostToDevice, h->stream));
+                next = N.cap;
+            }
+            count[d + 1] = d < path ? next : 0;
+            if (st) {
+                if (d > 0) st->secondary_rays += (uint64_t)n;
+                else st->primary_rays += (uint64_t)n;
+            }
+        }
+        for (int d = path; d >= 0; --d) {
+            const int64_t n = count[d];
+            if (n == 0) continue;
+            KTimer t(h, st, 3);
+            double* parent_child = d > 0 ? h->levels[d - 1].child : nullptr;
+            hipLaunchKernelGGL(k_combine, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->levels[d].rec, n,
+                               h->levels[d].surface, h->levels[d].child, parent_child, h->sample_col, h->S.materials,
+                               h->S.cfg.include_specular);
+            FRT_HIP(hipGetLastError());
+        }
+        {
+            KTimer t(h, st, 4);
+            hipLaunchKernelGGL(k_resolve, dim3(grid_for(bp)), dim3(kBlock), 0, h->stream, h->sample_col, bp, spp,
+                               dev_out + 4 * p0);
+            FRT_HIP(hipGetLastError());
+        }
+        if (st) {
+            FRT_HIP(hipStreamSynchronize(h->stream));
+        }
+    }
+    FRT_HIP(hipMemcpyAsync(host_counters, h->counters, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+    unsigned err = 0;
+    FRT_HIP(hipMemcpyAsync(&err, h->err, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+    if (st) (void)hipEventRecord(h->ev[1], h->stream);
+    FRT_HIP(hipStreamSynchronize(h->stream));
+    if (st) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
+        st->render_ms = ms;
+        st->pruned_secondary = host_counters[16];
+        st->errors = err;
+    }
+    if (err) {
+        char buf[128];
+        std::snprintf(buf, sizeof(buf), "render: device error bits 0x%x", err);
+        return fail(buf);
+    }
+    return 0;
+}
+
+int frt_render_rows_device(frt_scene_handle* h, const frt_frame_params* P, double* device_rgba, frt_frame_stats* st) {
+    if (!h || !P || !device_rgba) return fail("frt_render_rows_device: null argument");
+    return render_impl(h, P, device_rgba, st);
+}
+
+int frt_render_rows(frt_scene_handle* h, const frt_frame_params* P, double* host_rgba, frt_frame_stats* st) {
+    if (!h || !P || !host_rgba) return fail("frt_render_rows: null argument");
+    FRT_HIP(hipSetDevice(h->device));
+    const int64_t stride = P->row_stride > 0 ? P->row_stride : 1;
+    int64_t nrows = 0;
+    for (int64_t r = P->row_begin; r < P->row_end; r += stride) nrows++;
+    const int64_t n = nrows * h->S.cam.hsize * 4;
+    if (grow(&h->out_dev, h->out_cap, std::max<int64_t>(n, 4))) return -1;
+    int rc = render_impl(h, P, h->out_dev, st);
+    if (rc) return rc;
+    FRT_HIP(hipMemcpy(host_rgba, h->out_dev, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+}  // extern "C"

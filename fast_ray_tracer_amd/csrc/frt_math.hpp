@@ -1,0 +1,350 @@
+// frt-mi355x device math: binary64 vector helpers and the analytic
+// primitive tests, in the reference's operation order so that device results
+// match the reference bit for bit wherever only + - * / sqrt are involved.
+// Compiled with -ffp-contract=off (no FMA fusion), like the reference's
+// ISO-C build.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "frt_device.h"
+
+namespace frt {
+
+constexpr double kEps = 0.00001;       // reference linalg.h:7
+constexpr double kEqnEps = 1e-9;       // reference Roots3And4.c:36
+constexpr double kPi = 3.14159265358979323846;
+constexpr double k1Pi = 0.31830988618379067154;
+
+struct Ray {
+    double o[3];  // w = 1 implicitly
+    double d[3];  // w = 0 implicitly
+};
+
+struct Hit {
+    double t, u, v;
+    int node;
+};
+
+__device__ __forceinline__ bool feq(double a, double b) { return fabs(a - b) < kEps; }
+
+__device__ __forceinline__ double dot3(const double* a, const double* b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// vector_normalize (reference linalg.c:141-148): multiply by the reciprocal
+__device__ __forceinline__ void normalize3(const double* v, double* r) {
+    double inv = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    double x = v[0], y = v[1], z = v[2];
+    r[0] = x * inv;
+    r[1] = y * inv;
+    r[2] = z * inv;
+}
+
+__device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {
+    double x = a[1] * b[2] - a[2] * b[1];
+    double y = a[2] * b[0] - a[0] * b[2];
+    double z = a[0] * b[1] - a[1] * b[0];
+    r[0] = x;
+    r[1] = y;
+    r[2] = z;
+}
+
+// matrix_point_multiply with w = 1 (the m[i3]*1.0 term is exact)
+__device__ __forceinline__ void xf_point(const double* m, const double* p, double* r) {
+    double x = ((m[0] * p[0] + m[1] * p[1]) + m[2] * p[2]) + m[3];
+    double y = ((m[4] * p[0] + m[5] * p[1]) + m[6] * p[2]) + m[7];
+    double z = ((m[8] * p[0] + m[9] * p[1]) + m[10] * p[2]) + m[11];
+    r[0] = x;
+    r[1] = y;
+    r[2] = z;
+}
+
+// matrix_vector_multiply with w = +0 (kept: it can only change the sign of a zero)
+__device__ __forceinline__ void xf_vector(const double* m, const double* v, double* r) {
+    double x = ((m[0] * v[0] + m[1] * v[1]) + m[2] * v[2]) + m[3] * 0.0;
+    double y = ((m[4] * v[0] + m[5] * v[1]) + m[6] * v[2]) + m[7] * 0.0;
+    double z = ((m[8] * v[0] + m[9] * v[1]) + m[10] * v[2]) + m[11] * 0.0;
+    r[0] = x;
+    r[1] = y;
+    r[2] = z;
+}
+
+// transpose(m) * n with n.w = 0 (shape_normal_to_world, shapes.c:92-114)
+__device__ __forceinline__ void xf_normal_t(const double* m, const double* n, double* r) {
+    double x = ((m[0] * n[0] + m[4] * n[1]) + m[8] * n[2]) + m[12] * 0.0;
+    double y = ((m[1] * n[0] + m[5] * n[1]) + m[9] * n[2]) + m[13] * 0.0;
+    double z = ((m[2] * n[0] + m[6] * n[1]) + m[10] * n[2]) + m[14] * 0.0;
+    r[0] = x;
+    r[1] = y;
+    r[2] = z;
+}
+
+__device__ __forceinline__ Ray xf_ray(const double* m, const Ray& r) {
+    Ray t;
+    xf_point(m, r.o, t.o);
+    xf_vector(m, r.d, t.d);
+    return t;
+}
+
+// check_axis / bbox_check_axis (cube.c:16-53, bounding_box.c:124-162)
+__device__ __forceinline__ void slab(double o, double d, double lo, double hi, double& a, double& b) {
+    double nl = lo - o, nh = hi - o, t0, t1;
+    if (fabs(d) >= kEps) {
+        t0 = nl / d;
+        t1 = nh / d;
+    } else {
+        t0 = nl * __builtin_inf();
+        if (isnan(t0)) t0 = nl < 0 ? -__builtin_inf() : __builtin_inf();
+        t1 = nh * __builtin_inf();
+        if (isnan(t1)) t1 = nh < 0 ? -__builtin_inf() : __builtin_inf();
+    }
+    if (t0 > t1) {
+        a = t1;
+        b = t0;
+    } else {
+        a = t0;
+        b = t1;
+    }
+}
+
+__device__ __forceinline__ bool box_hit(const double* bb, const Ray& r) {
+    double x0, x1, y0, y1, z0, z1;
+    slab(r.o[0], r.d[0], bb[0], bb[3], x0, x1);
+    slab(r.o[1], r.d[1], bb[1], bb[4], y0, y1);
+    slab(r.o[2], r.d[2], bb[2], bb[5], z0, z1);
+    return fmax(fmax(x0, y0), z0) <= fmin(fmin(x1, y1), z1);
+}
+
+// ---- quartic (reference Roots3And4.c:43-244) ----
+__device__ __forceinline__ bool is_zero(double x) { return x > -kEqnEps && x < kEqnEps; }
+
+__device__ inline int solve_quadric(double c0, double c1, double c2, double* s) {
+    double p = c1 / (2 * c2);
+    double q = c0 / c2;
+    double D = p * p - q;
+    if (is_zero(D)) {
+        s[0] = -p;
+        return 1;
+    }
+    if (D < 0) return 0;
+    double sd = sqrt(D);
+    s[0] = sd - p;
+    s[1] = -sd - p;
+    return 2;
+}
+
+__device__ inline int solve_cubic(const double* c, double* s) {
+    double A = c[2] / c[3], B = c[1] / c[3], C = c[0] / c[3];
+    double sq_A = A * A;
+    double p = 1.0 / 3 * (-1.0 / 3 * sq_A + B);
+    double q = 1.0 / 2 * (2.0 / 27 * A * sq_A - 1.0 / 3 * A * B + C);
+    double cb_p = p * p * p;
+    double D = q * q + cb_p;
+    int num;
+    if (is_zero(D)) {
+        if (is_zero(q)) {
+            s[0] = 0;
+            num = 1;
+        } else {
+            double u = cbrt(-q);
+            s[0] = 2 * u;
+            s[1] = -u;
+            num = 2;
+        }
+    } else if (D < 0) {
+        double phi = 1.0 / 3 * acos(-q / sqrt(-cb_p));
+        double t = 2 * sqrt(-p);
+        s[0] = t * cos(phi);
+        s[1] = -t * cos(phi + kPi / 3);
+        s[2] = -t * cos(phi - kPi / 3);
+        num = 3;
+    } else {
+        double sd = sqrt(D);
+        double u = cbrt(sd - q);
+        double v = -cbrt(sd + q);
+        s[0] = u + v;
+        num = 1;
+    }
+    double sub = 1.0 / 3 * A;
+    for (int i = 0; i < num; ++i) s[i] -= sub;
+    return num;
+}
+
+__device__ __noinline__ int solve_quartic(const double* c, double* s) {
+    double coeffs[4];
+    double A = c[3] / c[4], B = c[2] / c[4], C = c[1] / c[4], D = c[0] / c[4];
+    double sq_A = A * A;
+    double p = -3.0 / 8 * sq_A + B;
+    double q = 1.0 / 8 * sq_A * A - 1.0 / 2 * A * B + C;
+    double r = -3.0 / 256 * sq_A * sq_A + 1.0 / 16 * sq_A * B - 1.0 / 4 * A * C + D;
+    int num;
+    if (is_zero(r)) {
+        coeffs[0] = q;
+        coeffs[1] = p;
+        coeffs[2] = 0;
+        coeffs[3] = 1;
+        num = solve_cubic(coeffs, s);
+        s[num++] = 0;
+    } else {
+        coeffs[0] = 1.0 / 2 * r * p - 1.0 / 8 * q * q;
+        coeffs[1] = -r;
+        coeffs[2] = -1.0 / 2 * p;
+        coeffs[3] = 1;
+        (void)solve_cubic(coeffs, s);
+        double z = s[0];
+        double u = z * z - r;
+        double v = 2 * z - p;
+        if (is_zero(u)) u = 0;
+        else if (u > 0) u = sqrt(u);
+        else return 0;
+        if (is_zero(v)) v = 0;
+        else if (v > 0) v = sqrt(v);
+        else return 0;
+        num = solve_quadric(z - u, q < 0 ? -v : v, 1, s);
+        num += solve_quadric(z + u, q < 0 ? v : -v, 1, s + num);
+    }
+    double sub = 1.0 / 4 * A;
+    for (int i = 0; i < num; ++i) s[i] -= sub;
+    return num;
+}
+
+// ---- primitive intersections: hits appended in the reference's emission order ----
+// Returns the number of hits written to h (<= 4).
+__device__ __forceinline__ int leaf_hits(const frt_node& nd, int ni, const double* __restrict__ prim,
+                                         const Ray& r, Hit* h) {
+    switch (nd.type) {
+    case FRT_SPHERE: {  // sphere.c:14-39
+        double a = dot3(r.d, r.d);
+        double b = 2 * dot3(r.d, r.o);
+        double c = dot3(r.o, r.o) - 1.0;
+        double disc = b * b - 4 * a * c;
+        if (disc < 0) return 0;
+        disc = sqrt(disc);
+        a = 1.0 / (2 * a);
+        h[0] = Hit{(-b - disc) * a, -1, -1, ni};
+        h[1] = Hit{(-b + disc) * a, -1, -1, ni};
+        return 2;
+    }
+    case FRT_CUBE: {  // cube.c:56-77
+        double x0, x1, y0, y1, z0, z1;
+        slab(r.o[0], r.d[0], -1, 1, x0, x1);
+        slab(r.o[1], r.d[1], -1, 1, y0, y1);
+        slab(r.o[2], r.d[2], -1, 1, z0, z1);
+        double tmin = fmax(fmax(x0, y0), z0), tmax = fmin(fmin(x1, y1), z1);
+        if (tmin > tmax) return 0;
+        h[0] = Hit{tmin, -1, -1, ni};
+        h[1] = Hit{tmax, -1, -1, ni};
+        return 2;
+    }
+    case FRT_PLANE:  // plane.c:11-24
+        if (fabs(r.d[1]) < kEps) return 0;
+        h[0] = Hit{-r.o[1] / r.d[1], -1, -1, ni};
+        return 1;
+    case FRT_TRIANGLE:
+    case FRT_SMOOTH_TRIANGLE: {  // triangle.c:11-44
+        const double* p = prim + nd.prim;
+        double dce2[3], p1o[3], oce1[3];
+        cross3(r.d, p + FRT_TRI_E2, dce2);
+        double det = dot3(p + FRT_TRI_E1, dce2);
+        if (fabs(det) < kEps) return 0;
+        double f = 1.0 / det;
+        p1o[0] = r.o[0] - p[0];
+        p1o[1] = r.o[1] - p[1];
+        p1o[2] = r.o[2] - p[2];
+        double u = f * dot3(p1o, dce2);
+        if (u < 0 || u > 1) return 0;
+        cross3(p1o, p + FRT_TRI_E1, oce1);
+        double v = f * dot3(r.d, oce1);
+        if (v < 0 || (u + v) > 1) return 0;
+        h[0] = Hit{f * dot3(p + FRT_TRI_E2, oce1), u, v, ni};
+        return 1;
+    }
+    case FRT_CYLINDER: {  // cylinder.c:11-87
+        const double* p = prim + nd.prim;
+        double mn = p[0], mx = p[1];
+        int n = 0;
+        double a = r.d[0] * r.d[0] + r.d[2] * r.d[2];
+        double b = 2 * (r.o[0] * r.d[0] + r.o[2] * r.d[2]);
+        double c = r.o[0] * r.o[0] + r.o[2] * r.o[2] - 1;
+        if (!feq(a, 0.0)) {
+            double disc = b * b - 4 * a * c;
+            if (disc < 0) return 0;
+            double sq = sqrt(disc);
+            double t0 = (-b - sq) / (2 * a), t1 = (-b + sq) / (2 * a);
+            if (t0 > t1) {
+                double tt = t0;
+                t0 = t1;
+                t1 = tt;
+            }
+            double y0 = r.o[1] + t0 * r.d[1];
+            if (mn <= y0 && y0 <= mx) h[n++] = Hit{t0, -1, -1, ni};
+            double y1 = r.o[1] + t1 * r.d[1];
+            if (mn <= y1 && y1 <= mx) h[n++] = Hit{t1, -1, -1, ni};
+        }
+        if (p[2] == 0.0 || feq(r.d[1], 0.0)) return n;
+        double ta = (mn - r.o[1]) / r.d[1];
+        double tb = (mx - r.o[1]) / r.d[1];
+        double xa = r.o[0] + ta * r.d[0], za = r.o[2] + ta * r.d[2];
+        if (xa * xa + za * za <= 1) h[n++] = Hit{ta, -1, -1, ni};
+        double xb = r.o[0] + tb * r.d[0], zb = r.o[2] + tb * r.d[2];
+        if (xb * xb + zb * zb <= 1) h[n++] = Hit{tb, -1, -1, ni};
+        return n;
+    }
+    case FRT_CONE: {  // cone.c:11-96
+        const double* p = prim + nd.prim;
+        double mn = p[0], mx = p[1];
+        int n = 0;
+        double a = r.d[0] * r.d[0] + r.d[2] * r.d[2] - r.d[1] * r.d[1];
+        double b = 2 * (r.o[0] * r.d[0] + r.o[2] * r.d[2] - r.o[1] * r.d[1]);
+        double c = r.o[0] * r.o[0] + r.o[2] * r.o[2] - r.o[1] * r.o[1];
+        if (feq(a, 0.0)) {
+            if (!feq(b, 0.0)) h[n++] = Hit{-c / (2 * b), -1, -1, ni};
+        } else {
+            double disc = b * b - 4 * a * c;
+            if (disc < 0) return 0;
+            double sq = sqrt(disc);
+            double t0 = (-b - sq) / (2 * a), t1 = (-b + sq) / (2 * a);
+            if (t0 > t1) {
+                double tt = t0;
+                t0 = t1;
+                t1 = tt;
+            }
+            double y0 = r.o[1] + t0 * r.d[1];
+            if (mn < y0 && y0 < mx) h[n++] = Hit{t0, -1, -1, ni};
+            double y1 = r.o[1] + t1 * r.d[1];
+            if (mn < y1 && y1 < mx) h[n++] = Hit{t1, -1, -1, ni};
+        }
+        if (p[2] == 0.0 || feq(r.d[1], 0.0)) return n;
+        double ta = (mn - r.o[1]) / r.d[1];
+        double xa = r.o[0] + ta * r.d[0], za = r.o[2] + ta * r.d[2];
+        if (xa * xa + za * za <= fabs(mn)) h[n++] = Hit{ta, -1, -1, ni};
+        double tb = (mx - r.o[1]) / r.d[1];
+        double xb = r.o[0] + tb * r.d[0], zb = r.o[2] + tb * r.d[2];
+        if (xb * xb + zb * zb <= fabs(mx)) h[n++] = Hit{tb, -1, -1, ni};
+        return n;
+    }
+    case FRT_TOROID: {  // toroid.c:15-52
+        const double* p = prim + nd.prim;
+        double r1 = p[0], r2 = p[1];
+        double ox = r.o[0], oy = r.o[1], oz = r.o[2];
+        double dx = r.d[0], dy = r.d[1], dz = r.d[2];
+        double sum_d_sq = dx * dx + dy * dy + dz * dz;
+        double e = ox * ox + oy * oy + oz * oz - r1 * r1 - r2 * r2;
+        double f = ox * dx + oy * dy + oz * dz;
+        double four_a_sq = 4.0 * r1 * r1;
+        double coeffs[5] = {e * e - four_a_sq * (r2 * r2 - oy * oy), 4.0 * f * e + 2.0 * four_a_sq * oy * dy,
+                            2.0 * sum_d_sq * e + 4.0 * f * f + four_a_sq * dy * dy, 4.0 * sum_d_sq * f,
+                            sum_d_sq * sum_d_sq};
+        double sol[4];
+        int n = solve_quartic(coeffs, sol);
+        for (int k = 0; k < n; ++k) h[k] = Hit{sol[n - 1 - k], -1, -1, ni};
+        return n;
+    }
+    default:
+        return 0;
+    }
+}
+
+}  // namespace frt

@@ -1,0 +1,28 @@
+/*
+ * frt-mi355x host API: render entry points.
+ *
+ * render_multi() is the drop-in boundary (reference src/renderer/renderer.h:46-47,
+ * called by generated main() at yaml_parser/yaml_parser.py:218). It flattens
+ * the scene and renders on MI355X through the device C-ABI declared in
+ * include/frt_device.h; there is no CPU fallback.
+ */
+#ifndef FRT_RENDERER_H
+#define FRT_RENDERER_H
+
+#include <stdbool.h>
+#include <stdlib.h>
+
+#include "../libs/linalg/linalg.h"
+#include "../libs/canvas/canvas.h"
+#include "../color/color.h"
+#include "../light/light.h"
+#include "../shapes/shapes.h"
+#include "../intersection/intersection.h"
+#include "world.h"
+#include "camera.h"
+#include "ray.h"
+
+Canvas render(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter);
+Canvas render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter);
+
+#endif

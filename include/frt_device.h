@@ -1,0 +1,220 @@
+/*
+ * frt_device.h — C ABI of the MI355X (gfx950) render engine.
+ *
+ * This is the thin boundary between the C11 host library (the drop-in
+ * scene API under fast_ray_tracer_amd/host/src/...) and the hand-written HIP
+ * kernels in fast_ray_tracer_amd/csrc. Plain structs, pointers and sizes only.
+ *
+ * What it replaces in the reference:
+ *   frt_render_rows / frt_render_rows_device  -> the body of
+ *       Canvas render_multi(Camera, World, size_t, size_t, bool)
+ *       (reference src/renderer/renderer.h:47, renderer.c:244-281): the
+ *       row-per-job pthread pool over per-thread deep world copies, and the
+ *       per-sample recursion color_at -> intersect_world -> shade_hit
+ *       (renderer.c:74-979, world.c:163-197).
+ *   frt_scene                                 -> the pointer-linked object
+ *       tree (struct shape, shapes.h:85-118), materials (material.h:196-220),
+ *       patterns (pattern.h:119-142), lights (light.h:57-76), camera
+ *       (camera.h:60-73) and config (config.h:56-62), flattened by
+ *       fast_ray_tracer_amd/host/frt_flatten.c.
+ *
+ * How the reference's render_multi binds to it: see INTEGRATION.md.
+ * All scene arithmetic is IEEE binary64, matching the reference.
+ */
+#ifndef FRT_DEVICE_H
+#define FRT_DEVICE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRT_ABI_VERSION 1u
+
+/* node kinds: same numbering as the reference's enum shape_enum (shapes.h:16-27) */
+enum frt_node_type {
+    FRT_CONE = 0,
+    FRT_CUBE = 1,
+    FRT_CYLINDER = 2,
+    FRT_PLANE = 3,
+    FRT_SMOOTH_TRIANGLE = 4,
+    FRT_SPHERE = 5,
+    FRT_TOROID = 6,
+    FRT_TRIANGLE = 7,
+    FRT_CSG = 8,
+    FRT_GROUP = 9
+};
+
+/*
+ * One node of the object tree in depth-first pre-order (the reference's child
+ * order, which its shadow-ray semantics depend on). A subtree occupies
+ * [index, skip). For a CSG node the left operand starts at index+1 and the
+ * right operand at right.
+ */
+typedef struct frt_node {
+    int32_t type;      /* enum frt_node_type */
+    int32_t skip;      /* first pre-order index after this subtree */
+    int32_t parent;    /* parent node, -1 for a world shape */
+    int32_t tparent;   /* nearest strict ancestor with a transform, -1 if none */
+    int32_t xform;     /* index into frt_scene.xforms (16 doubles, the inverse), -1 = identity */
+    int32_t material;  /* index into frt_scene.materials (leaves) */
+    int32_t prim;      /* offset into frt_scene.prim_data (leaves), CSG: operation (enum csg_ops_enum) */
+    int32_t right;     /* CSG: pre-order index of the right operand */
+    double bbox[6];    /* groups and CSG: own-space bounds min xyz, max xyz */
+} frt_node;
+
+/* per-leaf parameters in prim_data (doubles), by type:
+ *   cylinder / cone : minimum, maximum, closed
+ *   toroid          : r1, r2
+ *   triangle        : p1[3] e1[3] e2[3] normal[3] t1[2] t2[2] t3[2] use_textures
+ *   smooth triangle : p1[3] e1[3] e2[3] n1[3] n2[3] n3[3] t1[2] t2[2] t3[2] use_textures */
+#define FRT_TRI_P1 0
+#define FRT_TRI_E1 3
+#define FRT_TRI_E2 6
+#define FRT_TRI_N 9
+#define FRT_TRI_N2 12
+#define FRT_TRI_N3 15
+#define FRT_TRI_UV_FLAT 12
+#define FRT_TRI_UV_SMOOTH 18
+
+typedef struct frt_material {
+    double Ka[3], Kd[3], Ks[3], Tf[3], refl[3];
+    double Ns, Ni, Tr;
+    int32_t reflective;
+    int32_t casts_shadow;
+    /* pattern indices (frt_scene.patterns) or -1 */
+    int32_t map_Ka, map_Kd, map_Ks, map_Ns, map_d, map_bump, map_refl;
+    int32_t pad;
+} frt_material;
+
+/* pattern kinds: same numbering as the reference's enum pattern_type (pattern.h:23-41) */
+typedef struct frt_pattern {
+    int32_t type;
+    int32_t transform_identity;
+    int32_t uv_map;        /* texture map: enum uv_map_type */
+    int32_t faces;         /* texture map: index of the first face pattern */
+    int32_t child[3];      /* blended / nested / perturbed operands */
+    int32_t texture;       /* uv texture: index into frt_scene.textures */
+    int32_t width, height; /* uv checker */
+    int32_t octaves, seed; /* perturbed */
+    double inv[16];        /* inverse pattern transform */
+    double color[5][3];    /* a,b (concrete / uv check); main,ul,ur,bl,br (align check) */
+    double frequency, scale_factor, persistence;
+} frt_pattern;
+
+/* texture: texel (col,row) = canvas_pixel_at(canvas, col, row) pre-evaluated on the host
+ * (color-space function and optional 3x3 super-sampling applied), 3 doubles per texel */
+typedef struct frt_texture {
+    int64_t offset; /* into frt_scene.texels, in doubles */
+    int32_t width, height;
+} frt_texture;
+
+enum frt_light_type { FRT_AREA_LIGHT = 0, FRT_CIRCLE_LIGHT = 1, FRT_HEMISPHERE_LIGHT = 2, FRT_POINT_LIGHT = 3 };
+
+typedef struct frt_light {
+    int32_t type;
+    int32_t num_samples; /* points per cache row */
+    int32_t rows;        /* cache rows (reference cache_size), 1 for point lights */
+    int32_t pad;
+    int64_t points;      /* offset into frt_scene.light_points (3 doubles per point, row-major) */
+    double intensity[3];
+} frt_light;
+
+typedef struct frt_camera {
+    int64_t hsize, vsize, usteps, vsteps;
+    double half_width, half_height, pixel_size, canvas_distance;
+    double inv[16];          /* camera transform inverse */
+    double aperture_size;
+    int32_t aperture_type;   /* enum aperture_type (camera.h:9-19) */
+    int32_t jitter;          /* jittered CMJ sub-pixel tables */
+    double aperture_args[4];
+} frt_camera;
+
+typedef struct frt_config {
+    int32_t include_direct, include_ambient, include_diffuse, include_spec_highlight, include_specular;
+    int32_t path_length;
+    int32_t all_ni_one;      /* every material has Ni == 1.0: n1 = n2 = 1 without the container walk */
+    int32_t pad;
+} frt_config;
+
+typedef struct frt_scene {
+    uint32_t abi_version;
+    int32_t num_nodes;
+    const frt_node *nodes;
+    int32_t num_roots;       /* world shapes (generated main() has one: the divided world group) */
+    int32_t pad0;
+    const int32_t *roots;    /* pre-order index of each world shape */
+    int32_t num_xforms;
+    int32_t pad1;
+    const double *xforms;    /* 16 doubles per transform (the inverse matrix, row-major) */
+    int64_t prim_len;
+    const double *prim_data;
+    int32_t num_materials;
+    int32_t num_patterns;
+    const frt_material *materials;
+    const frt_pattern *patterns;
+    int32_t num_textures;
+    int32_t pad2;
+    const frt_texture *textures;
+    int64_t texel_len;       /* doubles */
+    const double *texels;
+    int32_t num_lights;
+    int32_t pad3;
+    const frt_light *lights;
+    int64_t light_point_len; /* doubles */
+    const double *light_points;
+    frt_camera camera;
+    const double *sample_table; /* usteps*vsteps*2: the non-jittered CMJ table (sampler.c:401-510) */
+    frt_config config;
+} frt_scene;
+
+typedef struct frt_scene_handle frt_scene_handle;
+
+typedef struct frt_frame_params {
+    int64_t row_begin, row_end; /* rows of the frame to render */
+    int64_t row_stride;         /* render rows row_begin, row_begin+stride, ... (1 = contiguous) */
+    uint64_t seed;              /* counter-RNG seed for stochastic rows (area-light cache rows, jitter) */
+    int64_t batch_samples;      /* camera samples per wavefront batch (0 = engine default) */
+    int32_t count_reference_rays; /* 1: also count the rays the reference would cast (slower) */
+    int32_t pad;
+} frt_frame_params;
+
+typedef struct frt_frame_stats {
+    uint64_t primary_rays;
+    uint64_t secondary_rays;      /* reflection / refraction rays actually traced */
+    uint64_t shadow_rays;         /* shadow rays actually traced */
+    uint64_t pruned_secondary;    /* zero-weight secondary rays not traced */
+    uint64_t hits;                /* path nodes shaded */
+    uint64_t errors;              /* capacity / depth overflows (non-zero = result invalid) */
+    double render_ms;             /* wall time of the device work (events) */
+    double kernel_ms[8];          /* per-kernel accumulated time: extend, shadow, shade, combine, resolve, gen */
+    uint64_t kernel_launches[8];
+    double shadow_kernel_bytes;   /* algorithmic bytes moved by the shadow kernel (DESIGN.md byte model) */
+} frt_frame_stats;
+
+/* number of HIP devices visible (0 when no GPU) */
+int frt_device_count(void);
+
+/* message of the last failing call on this thread */
+const char *frt_last_error(void);
+
+/* copy a flattened scene into HBM on `device`; the host scene may be freed afterwards */
+int frt_scene_upload(const frt_scene *scene, int device, frt_scene_handle **out);
+
+/* render rows into a host buffer (rows x hsize x 4 doubles, rows in the order rendered) */
+int frt_render_rows(frt_scene_handle *h, const frt_frame_params *params, double *host_rgba,
+                    frt_frame_stats *stats);
+
+/* same, writing into device memory on the handle's device (e.g. a torch tensor's storage) */
+int frt_render_rows_device(frt_scene_handle *h, const frt_frame_params *params, double *device_rgba,
+                           frt_frame_stats *stats);
+
+void frt_scene_release(frt_scene_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

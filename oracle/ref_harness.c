@@ -1,0 +1,42 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — linked into oracle/_ref/bin/* (the reference
+ * build), never into the product. The scene's main.c is compiled with
+ * -Drender_multi=frt_ref_render_multi; this wrapper calls the reference's own
+ * render_multi (reference src/renderer/renderer.c:244), times it, and dumps
+ * the raw canvas (width*height*4 doubles, row-major, row 0 = top).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
+
+#include "src/renderer/renderer.h"
+
+Canvas
+frt_ref_render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
+{
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    Canvas c = render_multi(cam, w, usteps, vsteps, jitter);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    double secs = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+
+    const char *canvas_path = getenv("FRT_REF_CANVAS");
+    if (canvas_path != NULL) {
+        FILE *f = fopen(canvas_path, "wb");
+        if (f != NULL) {
+            fwrite(c->arr, sizeof(Color), c->width * c->height, f);
+            fclose(f);
+        }
+    }
+    const char *stats_path = getenv("FRT_REF_STATS");
+    if (stats_path != NULL) {
+        FILE *f = fopen(stats_path, "w");
+        if (f != NULL) {
+            fprintf(f, "{\"render_multi_seconds\": %.9f, \"width\": %zu, \"height\": %zu, "
+                       "\"usteps\": %zu, \"vsteps\": %zu, \"threads\": %zu}\n",
+                    secs, c->width, c->height, usteps, vsteps, w->global_config->threading.num_threads);
+            fclose(f);
+        }
+    }
+    return c;
+}
