@@ -141,6 +141,12 @@ static struct {
 Canvas
 frt_capture_render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
 {
+    /* generated main() keeps global_config on its stack: keep a copy that outlives main() */
+    if (w != NULL && w->global_config != NULL) {
+        Global_config kept = (Global_config)malloc(sizeof(struct global_config));
+        *kept = *w->global_config;
+        w->global_config = kept;
+    }
     g_capture.cam = cam;
     g_capture.w = w;
     g_capture.usteps = usteps;
@@ -177,3 +183,15 @@ size_t frt_captured_vsteps(void) { return g_capture.vsteps; }
 int frt_captured_jitter(void) { return g_capture.jitter ? 1 : 0; }
 size_t frt_camera_hsize(Camera c) { return c->hsize; }
 size_t frt_camera_vsize(Camera c) { return c->vsize; }
+
+/* Put glibc's drand48() / rand() streams back into their fresh-process state
+ * (drand48 state 0 with the default multiplier, rand() seeded with 1), so a
+ * scene built inside a long-lived process draws the same jittered light
+ * caches as the reference's one-shot executable does. */
+void
+frt_reset_libc_rng(void)
+{
+    unsigned short zero[3] = {0, 0, 0};
+    seed48(zero);
+    srand(1);
+}

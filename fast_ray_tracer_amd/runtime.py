@@ -1,0 +1,177 @@
+"""ctypes bindings for the frt-mi355x host and device libraries.
+
+A scene is a codegen main.c (``yaml_parser.py scene.yml > main.c``) compiled
+unchanged in capture mode (``build.build_scene``): running its ``main`` builds
+the scene through the drop-in C API and hands the Camera / World to
+``frt_capture_render_multi`` instead of rendering. ``GpuRenderer`` then
+flattens the captured scene once, uploads it to HBM and renders rows with the
+HIP engine (``include/frt_device.h``). There is no CPU fallback: if
+libfrt_device.so or a GPU is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from . import build
+
+_lock = threading.Lock()
+_host = None
+
+
+class FrameParams(ctypes.Structure):
+    _fields_ = [("row_begin", ctypes.c_int64), ("row_end", ctypes.c_int64), ("row_stride", ctypes.c_int64),
+                ("seed", ctypes.c_uint64), ("batch_samples", ctypes.c_int64),
+                ("count_reference_rays", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class FrameStats(ctypes.Structure):
+    _fields_ = [("primary_rays", ctypes.c_uint64), ("secondary_rays", ctypes.c_uint64),
+                ("shadow_rays", ctypes.c_uint64), ("pruned_secondary", ctypes.c_uint64),
+                ("hits", ctypes.c_uint64), ("errors", ctypes.c_uint64), ("render_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_uint64 * 8),
+                ("shadow_kernel_bytes", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        names = ["extend", "shadow", "shade", "combine", "resolve", "primary", "k6", "k7"]
+        return {
+            "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
+            "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
+            "hits": int(self.hits), "errors": int(self.errors), "render_ms": float(self.render_ms),
+            "kernel_ms": {names[i]: float(self.kernel_ms[i]) for i in range(8) if self.kernel_launches[i]},
+            "kernel_launches": {names[i]: int(self.kernel_launches[i]) for i in range(8) if self.kernel_launches[i]},
+        }
+
+
+def host_lib(auto_build: bool = False) -> ctypes.CDLL:
+    """Load libfrt_host.so (which pulls in libfrt_device.so) with global symbols."""
+    global _host
+    with _lock:
+        if _host is not None:
+            return _host
+        if auto_build:
+            build.build_host()
+        if not os.path.exists(build.HOST_LIB) or not os.path.exists(build.DEVICE_LIB):
+            raise RuntimeError("frt native libraries are not built: run __graft_entry__.build() "
+                               "(expected %s and %s)" % (build.HOST_LIB, build.DEVICE_LIB))
+        lib = ctypes.CDLL(build.HOST_LIB, mode=ctypes.RTLD_GLOBAL)
+        vp = ctypes.c_void_p
+        lib.frt_captured.restype = ctypes.c_int
+        for fn in ("frt_captured_camera", "frt_captured_world"):
+            getattr(lib, fn).restype = vp
+        for fn in ("frt_captured_usteps", "frt_captured_vsteps"):
+            getattr(lib, fn).restype = ctypes.c_size_t
+        lib.frt_captured_jitter.restype = ctypes.c_int
+        lib.frt_camera_hsize.restype = ctypes.c_size_t
+        lib.frt_camera_hsize.argtypes = [vp]
+        lib.frt_camera_vsize.restype = ctypes.c_size_t
+        lib.frt_camera_vsize.argtypes = [vp]
+        lib.frt_host_prepare.restype = vp
+        lib.frt_host_prepare.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool, ctypes.c_int]
+        lib.frt_host_last_error.restype = ctypes.c_char_p
+        lib.frt_device_count.restype = ctypes.c_int
+        lib.frt_last_error.restype = ctypes.c_char_p
+        lib.frt_render_rows.restype = ctypes.c_int
+        lib.frt_render_rows.argtypes = [vp, ctypes.POINTER(FrameParams), vp, ctypes.POINTER(FrameStats)]
+        lib.frt_render_rows_device.restype = ctypes.c_int
+        lib.frt_render_rows_device.argtypes = [vp, ctypes.POINTER(FrameParams), vp, ctypes.POINTER(FrameStats)]
+        lib.frt_scene_release.argtypes = [vp]
+        _host = lib
+        return lib
+
+
+class Scene:
+    """A scene built by running a capture-mode generated main.c."""
+
+    def __init__(self, scene_so: str, asset_root: str | None = None):
+        lib = host_lib()
+        self._so = ctypes.CDLL(scene_so, mode=ctypes.RTLD_GLOBAL)
+        self._so.frt_scene_main.restype = ctypes.c_int
+        cwd = os.getcwd()
+        lib.frt_reset_libc_rng()
+        try:
+            if asset_root:
+                os.chdir(asset_root)
+            rc = self._so.frt_scene_main()
+        finally:
+            os.chdir(cwd)
+        if rc != 0 or not lib.frt_captured():
+            raise RuntimeError("scene main() did not reach render_multi (rc=%d): %s" % (rc, scene_so))
+        self.camera = lib.frt_captured_camera()
+        self.world = lib.frt_captured_world()
+        self.usteps = int(lib.frt_captured_usteps())
+        self.vsteps = int(lib.frt_captured_vsteps())
+        self.jitter = bool(lib.frt_captured_jitter())
+        self.width = int(lib.frt_camera_hsize(self.camera))
+        self.height = int(lib.frt_camera_vsize(self.camera))
+        self.name = os.path.splitext(os.path.basename(scene_so))[0]
+
+    @property
+    def spp(self) -> int:
+        return self.usteps * self.vsteps
+
+
+class GpuRenderer:
+    """render_multi's device path for one captured scene on one HIP device."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        self.lib = host_lib()
+        if self.lib.frt_device_count() <= 0:
+            raise RuntimeError("frt: no HIP device visible; the GPU path has no CPU fallback")
+        self.scene = scene
+        self.device = device
+        h = self.lib.frt_host_prepare(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter, device)
+        if not h:
+            raise RuntimeError("frt: scene upload failed: " + self.lib.frt_host_last_error().decode())
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.lib.frt_scene_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _params(self, row_begin, row_end, row_stride, seed, batch_samples):
+        p = FrameParams()
+        p.row_begin = row_begin
+        p.row_end = self.scene.height if row_end is None else row_end
+        p.row_stride = row_stride
+        p.seed = seed
+        p.batch_samples = batch_samples
+        return p
+
+    @staticmethod
+    def rows_in(row_begin, row_end, row_stride) -> int:
+        return len(range(row_begin, row_end, row_stride))
+
+    def render(self, row_begin: int = 0, row_end: int | None = None, row_stride: int = 1, seed: int = 0x5EED,
+               batch_samples: int = 0, stats: bool = False):
+        """Render rows into a host array (rows, width, 4) float64."""
+        p = self._params(row_begin, row_end, row_stride, seed, batch_samples)
+        n = self.rows_in(p.row_begin, p.row_end, row_stride)
+        out = np.zeros((n, self.scene.width, 4), dtype=np.float64)
+        st = FrameStats()
+        rc = self.lib.frt_render_rows(self.handle, ctypes.byref(p), out.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.byref(st) if stats else None)
+        if rc != 0:
+            raise RuntimeError("frt render failed: " + self.lib.frt_last_error().decode())
+        return (out, st) if stats else out
+
+    def render_into(self, device_ptr: int, row_begin: int = 0, row_end: int | None = None, row_stride: int = 1,
+                    seed: int = 0x5EED, batch_samples: int = 0, stats: bool = False):
+        """Render rows into device memory (e.g. a torch.cuda tensor's data_ptr())."""
+        p = self._params(row_begin, row_end, row_stride, seed, batch_samples)
+        st = FrameStats()
+        rc = self.lib.frt_render_rows_device(self.handle, ctypes.byref(p), ctypes.c_void_p(device_ptr),
+                                             ctypes.byref(st) if stats else None)
+        if rc != 0:
+            raise RuntimeError("frt render failed: " + self.lib.frt_last_error().decode())
+        return st if stats else None

@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden from the REAL reference.
+
+Run in the build container only (needs /root/reference). For every entry of
+SCENES it:
+
+  1. loads the reference scene YAML, applies the listed overrides (image size,
+     single-row area-light caches, GI off, output path) and writes it to a
+     scratch directory;
+  2. runs the reference's own codegen (yaml_parser/yaml_parser.py, from a
+     scratch copy of /root/reference) to produce main.c, saved as
+     tests/golden/scenes/<name>.c (an input fixture: the program the drop-in
+     boundary must accept unchanged);
+  3. builds the reference renderer around it (oracle/build_ref.sh ->
+     oracle/_ref/bin/<name>), runs it, and stores the raw canvas
+     (float64, width x height x 3) plus the sha256 of its 16-bit PPM and PNG
+     as tests/golden/<name>.npz / golden.json (expected outputs).
+
+Scene assets the scenes load at run time (OBJ meshes, PNG textures) are
+copied as data into tests/golden/assets/ with their relative paths, so the
+tests run on a machine without /root/reference.
+"""
+from __future__ import annotations
+
+import copy
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+import numpy as np
+import yaml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("FRT_REFERENCE_DIR", "/root/reference")
+SCRATCH = "/tmp/frt_golden"
+REF_COPY = os.path.join(SCRATCH, "ref")
+
+# name -> (yaml, overrides, golden canvas kind)
+#   size: (w, h); steps: (u, v); cache: area-light cache-size; threads: reference pool size
+SCENES = {
+    "checkered_sphere_200": ("scenes/checkered_sphere/checkered_sphere.yml", {"size": (200, 200)}),
+    "checkered_sphere_800": ("scenes/checkered_sphere/checkered_sphere.yml", {"size": (800, 800), "hash_only": True}),
+    "bounding_boxes_200x80": ("scenes/bounding_boxes/bounding_boxes.yml", {"size": (200, 80)}),
+    "cornell_direct_64_4x4": ("scenes/cornell_box/cornell_box.yml", {"size": (64, 64), "cache": 1, "gi_off": True}),
+    "cornell_direct_128_1x1": ("scenes/cornell_box/cornell_box.yml",
+                               {"size": (128, 128), "steps": (1, 1), "cache": 1, "gi_off": True}),
+    "checkered_cube_160x80": ("scenes/checkered_cube/checkered_cube.yml", {"size": (160, 80)}),
+    "checkered_cylinder_120": ("scenes/checkered_cylinder/checkered_cylinder.yml", {"size": (120, 120)}),
+    "checkered_torus_120": ("scenes/checkered_torus/checkered_torus.yml", {"size": (120, 120)}),
+    "align_check_plane_120": ("scenes/align_check_plane/align_check_plane.yml", {"size": (120, 120)}),
+    "group_test_150x50": ("scenes/group_test/group.yml", {"size": (150, 50)}),
+    "shadow_glamour_150x60": ("scenes/shadow_glamour_shot/shadow_glamour_shot.yml", {"size": (150, 60), "cache": 1}),
+    "test_scene_120": ("scenes/test/test.yml", {"size": (120, 120)}),
+    "teapot_low_100": ("scenes/teapot/teapot.yml", {"size": (100, 100)}),
+    "area_light_test_100": ("scenes/area_light_test/area_light_test.yml", {"size": (100, 100), "cache": 1}),
+    "reflect_refract_160x80": ("scenes/reflect_refract/reflect_refract.yml", {"size": (160, 80)}),
+    "bump_map_100": ("scenes/bump_map_test/bump_map_test.yml", {"size": (100, 100)}),
+    # benchmark scene (BASELINE.json configs[2]: cornell_box 800x800, 4x4 CMJ, full recursion;
+    # GI off, single-row area-light cache = the deterministic parity variant). No canvas golden:
+    # the reference takes minutes here; parity is checked at the small sizes above.
+    "cornell_direct_800_4x4": ("scenes/cornell_box/cornell_box.yml",
+                               {"size": (800, 800), "cache": 1, "gi_off": True, "no_golden": True}),
+}
+
+
+def find(items, pred):
+    return [it for it in items if isinstance(it, dict) and pred(it)]
+
+
+def apply_overrides(tree, name, ov):
+    cams = find(tree, lambda it: it.get("add") == "camera")
+    for cam in cams:
+        if "size" in ov:
+            cam["width"], cam["height"] = ov["size"]
+        if "steps" in ov:
+            cam["usteps"], cam["vsteps"] = ov["steps"]
+            ap = cam.setdefault("aperture", {})
+            ap["usteps"], ap["vsteps"] = ov["steps"]
+    if "cache" in ov:
+        for light in find(tree, lambda it: it.get("add") == "light" and ("corner" in it or "radius" in it)):
+            light["cache-size"] = ov["cache"]
+    cfgs = find(tree, lambda it: it.get("add") == "config")
+    if not cfgs:
+        cfg = {"add": "config"}
+        tree.insert(0, cfg)
+        cfgs = [cfg]
+    cfg = cfgs[0]
+    cfg.setdefault("threading", {})["thread-count"] = ov.get("threads", 8)
+    cfg.setdefault("output", {})["file"] = os.path.join(SCRATCH, "out", name)
+    if ov.get("gi_off"):
+        ill = cfg.setdefault("illumination", {})
+        ill["include-global"] = False
+        ill.setdefault("global-illumination", {})["photon-count"] = 0
+    return tree
+
+
+def sha256(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def assets_of(main_c_text):
+    out = set()
+    for line in main_c_text.splitlines():
+        if "access(\"" in line:
+            out.add(line.split("access(\"", 1)[1].split("\"", 1)[0])
+    return sorted(out)
+
+
+def main(names):
+    if not os.path.isdir(os.path.join(REF, "src")):
+        sys.exit("reference not found at " + REF)
+    os.makedirs(os.path.join(SCRATCH, "out"), exist_ok=True)
+    if not os.path.isdir(REF_COPY):
+        shutil.copytree(REF, REF_COPY)
+        subprocess.run(["chmod", "-R", "u+w", REF_COPY], check=True)
+    scenes_dir = os.path.join(HERE, "scenes")
+    assets_dir = os.path.join(HERE, "assets")
+    os.makedirs(scenes_dir, exist_ok=True)
+    index_path = os.path.join(HERE, "golden.json")
+    index = json.load(open(index_path)) if os.path.exists(index_path) else {}
+
+    for name in names:
+        yml_rel, ov = SCENES[name]
+        with open(os.path.join(REF_COPY, yml_rel)) as f:
+            tree = yaml.safe_load(f)
+        tree = apply_overrides(copy.deepcopy(tree), name, ov)
+        yml_out = os.path.join(SCRATCH, name + ".yml")
+        with open(yml_out, "w") as f:
+            yaml.safe_dump(tree, f, sort_keys=False)
+        gen = subprocess.run([sys.executable, "yaml_parser/yaml_parser.py", yml_out], cwd=REF_COPY,
+                             capture_output=True, text=True)
+        if gen.returncode != 0:
+            print("codegen failed for", name, gen.stderr[-2000:])
+            continue
+        main_c = os.path.join(scenes_dir, name + ".c")
+        with open(main_c, "w") as f:
+            f.write(gen.stdout)
+        for asset in assets_of(gen.stdout):
+            dst = os.path.join(assets_dir, asset)
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            shutil.copyfile(os.path.join(REF_COPY, asset), dst)
+            mtl = asset[:-3] + "mtl"
+            if asset.endswith(".obj") and os.path.exists(os.path.join(REF_COPY, mtl)):
+                shutil.copyfile(os.path.join(REF_COPY, mtl), os.path.join(assets_dir, mtl))
+        entry = {"yaml": yml_rel, "overrides": {k: v for k, v in ov.items()}}
+        if ov.get("no_golden"):
+            index[name] = entry
+            print(name, "main.c only")
+            continue
+        b = subprocess.run(["bash", os.path.join(ROOT, "oracle", "build_ref.sh"), main_c, name],
+                           capture_output=True, text=True)
+        if b.returncode != 0:
+            print("reference build failed for", name, b.stderr[-2000:])
+            continue
+        binary = b.stdout.strip().splitlines()[-1]
+        canvas_bin = os.path.join(SCRATCH, name + ".canvas")
+        stats_json = os.path.join(SCRATCH, name + ".stats.json")
+        env = dict(os.environ, FRT_REF_CANVAS=canvas_bin, FRT_REF_STATS=stats_json)
+        t0 = time.time()
+        r = subprocess.run([binary], cwd=REF_COPY, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        if r.returncode != 0:
+            print("reference run failed for", name, r.stderr[-2000:])
+            continue
+        stats = json.load(open(stats_json))
+        w, h = stats["width"], stats["height"]
+        canvas = np.fromfile(canvas_bin, dtype=np.float64).reshape(h, w, 4)[:, :, :3]
+        out_base = os.path.join(SCRATCH, "out", name)
+        entry.update({
+            "width": w, "height": h, "usteps": stats["usteps"], "vsteps": stats["vsteps"],
+            "ref_threads": stats["threads"], "ref_render_multi_seconds": stats["render_multi_seconds"],
+            "ppm_sha256": sha256(out_base + ".ppm"), "png_sha256": sha256(out_base + ".png"),
+            "canvas_sum": [float(x) for x in canvas.reshape(-1, 3).sum(axis=0)],
+        })
+        if not ov.get("hash_only"):
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), canvas=canvas)
+            entry["canvas"] = name + ".npz"
+        index[name] = entry
+        print("%-28s %4dx%-4d %.2fs (wall %.1fs)" % (name, w, h, stats["render_multi_seconds"], time.time() - t0))
+        with open(index_path, "w") as f:
+            json.dump(index, f, indent=1, sort_keys=True)
+    with open(index_path, "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(SCENES))
