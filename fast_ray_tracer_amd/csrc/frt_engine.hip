@@ -113,6 +113,7 @@ __device__ void shade_prepare(const DevScene& S, const Batch& B, const Ray& r, c
                               unsigned long long* counters, unsigned* err) {
     Comps c;
     prepare(S, r, h, c);
+    atomicAdd(counters + 1, 1ull);  // shaded path nodes
     const frt_material& M = S.materials[c.material];
     NodeRec nr;
     for (int k = 0; k < 3; ++k) {
@@ -494,6 +495,13 @@ struct frt_scene_handle {
     unsigned long long* counters = nullptr;  // [0..15] queue counts per level, [16] pruned
     unsigned* err = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
+    struct Mark {
+        int slot;
+        size_t a, b;
+    };
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<Mark> ev_marks;
+    size_t ev_used = 0;
 };
 
 static thread_local std::string g_last_error;
@@ -628,6 +636,7 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->out_dev));
     hip_ignore(hipFree(h->counters));
     hip_ignore(hipFree(h->err));
+    for (hipEvent_t e : h->ev_pool) hip_ignore(hipEventDestroy(e));
     if (h->ev[0]) hip_ignore(hipEventDestroy(h->ev[0]));
     if (h->ev[1]) hip_ignore(hipEventDestroy(h->ev[1]));
     if (h->stream) hip_ignore(hipStreamDestroy(h->stream));
@@ -659,31 +668,46 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + frt::kBlock - 1) / frt::kBlock); }
 
+// Kernel timing without host synchronisation: events are recorded around each
+// launch on the engine stream and read back once the frame has completed.
 struct KTimer {
     frt_scene_handle* h;
     frt_frame_stats* st;
     int slot;
-    hipEvent_t a = nullptr, b = nullptr;
+    size_t a = 0;
+    static hipEvent_t event(frt_scene_handle* h, size_t i) {
+        while (h->ev_pool.size() <= i) {
+            hipEvent_t e;
+            hip_ignore(hipEventCreate(&e));
+            h->ev_pool.push_back(e);
+        }
+        return h->ev_pool[i];
+    }
     KTimer(frt_scene_handle* h_, frt_frame_stats* st_, int slot_) : h(h_), st(st_), slot(slot_) {
         if (st) {
-            (void)hipEventCreate(&a);
-            (void)hipEventCreate(&b);
-            (void)hipEventRecord(a, h->stream);
+            a = h->ev_used++;
+            hip_ignore(hipEventRecord(event(h, a), h->stream));
         }
     }
     ~KTimer() {
         if (st) {
-            (void)hipEventRecord(b, h->stream);
-            (void)hipEventSynchronize(b);
-            float ms = 0.f;
-            (void)hipEventElapsedTime(&ms, a, b);
-            st->kernel_ms[slot] += ms;
-            st->kernel_launches[slot] += 1;
-            (void)hipEventDestroy(a);
-            (void)hipEventDestroy(b);
+            size_t b = h->ev_used++;
+            hip_ignore(hipEventRecord(event(h, b), h->stream));
+            h->ev_marks.push_back({slot, a, b});
         }
     }
 };
+
+static void collect_timings(frt_scene_handle* h, frt_frame_stats* st) {
+    for (const auto& m : h->ev_marks) {
+        float ms = 0.f;
+        hip_ignore(hipEventElapsedTime(&ms, h->ev_pool[m.a], h->ev_pool[m.b]));
+        st->kernel_ms[m.slot] += ms;
+        st->kernel_launches[m.slot] += 1;
+    }
+    h->ev_marks.clear();
+    h->ev_used = 0;
+}
 
 static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
     using namespace frt;
@@ -789,9 +813,6 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
                                dev_out + 4 * p0);
             FRT_HIP(hipGetLastError());
         }
-        if (st) {
-            FRT_HIP(hipStreamSynchronize(h->stream));
-        }
     }
     FRT_HIP(hipMemcpyAsync(host_counters, h->counters, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
     unsigned err = 0;
@@ -803,7 +824,10 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
         st->render_ms = ms;
         st->pruned_secondary = host_counters[16];
+        st->hits = host_counters[17];
+        st->shadow_rays = h->S.cfg.include_direct ? host_counters[17] * (uint64_t)h->samples_per_node : 0;
         st->errors = err;
+        collect_timings(h, st);
     }
     if (err) {
         char buf[128];

@@ -389,3 +389,24 @@ done:
     free(buffer);
     return code;
 }
+
+/* Encode a raw rgba canvas (width*height*4 doubles) exactly as write_ppm_file
+ * would; used by tests and bench.py to compare PPM bytes without touching the
+ * file system. Returns the byte count, writes into out when it is large enough. */
+size_t
+frt_encode_ppm(const double *rgba, size_t width, size_t height, int use_scaling, unsigned char *out, size_t cap)
+{
+    struct canvas c;
+    c.arr = (Color *)rgba;
+    c.width = width;
+    c.height = height;
+    c.super_sample = false;
+    c.color_space_fn = NULL;
+    Ppm p = construct_ppm(&c, use_scaling != 0);
+    size_t n = p->len;
+    if (out != NULL && cap >= n) {
+        memcpy(out, p->arr, n);
+    }
+    ppm_free(p);
+    return n;
+}

@@ -79,6 +79,8 @@ def host_lib(auto_build: bool = False) -> ctypes.CDLL:
         lib.frt_render_rows_device.restype = ctypes.c_int
         lib.frt_render_rows_device.argtypes = [vp, ctypes.POINTER(FrameParams), vp, ctypes.POINTER(FrameStats)]
         lib.frt_scene_release.argtypes = [vp]
+        lib.frt_encode_ppm.restype = ctypes.c_size_t
+        lib.frt_encode_ppm.argtypes = [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, vp, ctypes.c_size_t]
         _host = lib
         return lib
 
@@ -175,3 +177,19 @@ class GpuRenderer:
         if rc != 0:
             raise RuntimeError("frt render failed: " + self.lib.frt_last_error().decode())
         return st if stats else None
+
+
+def encode_ppm(rgba: np.ndarray, use_scaling: bool = True) -> bytes:
+    """16-bit P6 PPM bytes of a (h, w, 3|4) float64 canvas, encoded by the host
+    library exactly as write_ppm_file(c, use_scaling, path) writes them."""
+    lib = host_lib()
+    h, w = rgba.shape[:2]
+    buf = np.zeros((h, w, 4), dtype=np.float64)
+    buf[:, :, :rgba.shape[2]] = rgba[:, :, :min(4, rgba.shape[2])]
+    if rgba.shape[2] == 3:
+        buf[:, :, 3] = 0.0
+    n = lib.frt_encode_ppm(buf.ctypes.data_as(ctypes.c_void_p), w, h, int(use_scaling), None, 0)
+    out = np.zeros(n, dtype=np.uint8)
+    lib.frt_encode_ppm(buf.ctypes.data_as(ctypes.c_void_p), w, h, int(use_scaling),
+                       out.ctypes.data_as(ctypes.c_void_p), n)
+    return out.tobytes()

@@ -1,0 +1,55 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+if ORACLE_DIR not in sys.path:
+    sys.path.insert(0, ORACLE_DIR)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+ASSETS = os.path.join(GOLDEN, "assets")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP engine)")
+
+
+def golden_index():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+def canvas_goldens():
+    return sorted(n for n, e in golden_index().items() if "canvas" in e)
+
+
+@pytest.fixture(scope="session")
+def built():
+    from fast_ray_tracer_amd import build
+    build.build_host()
+    build.build_oracle()
+    return build
+
+
+_scenes = {}
+
+
+def load_scene(name):
+    """Capture a golden scene (built once per session)."""
+    if name not in _scenes:
+        from fast_ray_tracer_amd import build
+        from fast_ray_tracer_amd.runtime import Scene
+        so = build.build_scene(os.path.join(GOLDEN, "scenes", name + ".c"))
+        _scenes[name] = Scene(so, asset_root=ASSETS)
+    return _scenes[name]
+
+
+def load_golden_canvas(name):
+    import numpy as np
+    e = golden_index()[name]
+    return np.load(os.path.join(GOLDEN, e["canvas"]))["canvas"]

@@ -65,6 +65,11 @@ SCENES = {
     # the reference takes minutes here; parity is checked at the small sizes above.
     "cornell_direct_800_4x4": ("scenes/cornell_box/cornell_box.yml",
                                {"size": (800, 800), "cache": 1, "gi_off": True, "no_golden": True}),
+    # bench.py's cpu_baseline sample: the same scene at 200x200 (1/16 of the pixels), the
+    # reference's own pthread pool with 16 threads (the GPU box's CPU share)
+    "cornell_direct_200_4x4_t16": ("scenes/cornell_box/cornell_box.yml",
+                                   {"size": (200, 200), "cache": 1, "gi_off": True, "threads": 16,
+                                    "ref_binary_only": True}),
 }
 
 
@@ -157,6 +162,10 @@ def main(names):
                            capture_output=True, text=True)
         if b.returncode != 0:
             print("reference build failed for", name, b.stderr[-2000:])
+            continue
+        if ov.get("ref_binary_only"):
+            index[name] = entry
+            print(name, "main.c + reference binary")
             continue
         binary = b.stdout.strip().splitlines()[-1]
         canvas_bin = os.path.join(SCRATCH, name + ".canvas")
