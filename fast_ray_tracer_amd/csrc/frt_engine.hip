@@ -4,9 +4,10 @@
 // reflected_color, refracted_color} (renderer.c:348-827) is unrolled into
 // depth levels. For one batch of camera samples:
 //
-//   k_primary  (level 0)  camera ray -> closest hit -> prepare_computations,
-//                         spawn reflection / refraction rays into queue 1
-//   k_extend   (level d)  queued ray -> closest hit -> prepare, spawn into d+1
+//   k_trace    (level d)  camera ray (d = 0) or queued ray -> closest hit
+//                         (ordered BVH/CSG walk, per-lane state in LDS)
+//   k_prepare  (level d)  prepare_computations, spawn reflection /
+//                         refraction rays into queue d+1
 //   k_shadow   (level d)  one lane per (hit, light sample): ordered any-hit
 //                         walk; unshadowed counts reduced per wave, one
 //                         integer atomic per (hit, light) segment
@@ -106,11 +107,81 @@ __device__ __forceinline__ void ray_for_pixel(const frt_camera& cam, double px, 
     normalize3(v, r.d);
 }
 
-// shared tail of k_primary / k_extend: prepare, record, spawn children
-__device__ void shade_prepare(const DevScene& S, const Batch& B, const Ray& r, const Hit& h, int64_t node,
-                              uint64_t key, int32_t parent, int32_t slot, NodeRec* __restrict__ rec,
-                              QueuedRay* __restrict__ next_q, int64_t next_cap, unsigned long long* next_count,
-                              unsigned long long* counters, unsigned* err) {
+// camera ray of sample s of a batch (k_trace level 0 and k_prepare level 0)
+__device__ __forceinline__ void camera_ray(const DevScene& S, const Batch& B, int64_t s, Ray& r, uint64_t& key) {
+    const int64_t pix = B.pixel_begin + s / B.spp;
+    const int sub = (int)(s % B.spp);
+    const int64_t hs = S.cam.hsize;
+    const int64_t row = B.row_begin + (pix / hs) * B.row_stride;
+    const int64_t col = pix % hs;
+    ray_for_pixel(S.cam, (double)col, (double)row, S.sample_table + 2 * sub, r);  // sub = v*usteps + u
+    const uint64_t global_sample = (uint64_t)((row * hs + col) * B.spp + sub);
+    key = (global_sample << 12) | 1ull;
+}
+
+struct HitRec {
+    double t;
+    int32_t node;  // -1: miss
+    int32_t pad;
+};
+
+extern __shared__ __align__(16) char frt_walk_smem[];
+
+// closest hit of every ray of one level (level 0: camera rays generated in place)
+template <int kFeat>
+__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
+                                                       HitRec* __restrict__ hits, unsigned* err) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r;
+    if (q == nullptr) {
+        uint64_t key;
+        camera_ray(S, B, i, r, key);
+    } else {
+        const QueuedRay& qr = q[i];
+        for (int k = 0; k < 3; ++k) {
+            r.o[k] = qr.o[k];
+            r.d[k] = qr.d[k];
+        }
+    }
+    unsigned e = 0;
+    double t;
+    const int node = walk<false, kFeat>(S, r, 0.0, t, frt_walk_smem, e);
+    hits[i] = HitRec{t, node, 0};
+    if (e) atomicOr(err, e);
+}
+
+// prepare_computations + spawn of the reflection / refraction rays (renderer.c:369-605)
+__global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
+                                                    const HitRec* __restrict__ hits, NodeRec* __restrict__ rec,
+                                                    QueuedRay* __restrict__ next_q, int64_t next_cap,
+                                                    unsigned long long* next_count, unsigned long long* counters,
+                                                    unsigned* err) {
+    const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (node >= n) return;
+    Ray r;
+    uint64_t key;
+    int32_t parent = -1, slot = 0;
+    if (q == nullptr) {
+        camera_ray(S, B, node, r, key);
+    } else {
+        const QueuedRay& qr = q[node];
+        for (int k = 0; k < 3; ++k) {
+            r.o[k] = qr.o[k];
+            r.d[k] = qr.d[k];
+        }
+        key = qr.key;
+        parent = qr.parent;
+        slot = qr.slot;
+    }
+    const HitRec hr = hits[node];
+    if (hr.node < 0) {
+        rec[node].material = -1;
+        rec[node].parent = parent;
+        rec[node].slot = slot;
+        return;
+    }
+    Hit h{hr.t, -1, -1, hr.node};
     Comps c;
     prepare(S, r, h, c);
     atomicAdd(counters + 1, 1ull);  // shaded path nodes
@@ -166,15 +237,15 @@ __device__ void shade_prepare(const DevScene& S, const Batch& B, const Ray& r, c
         if (reflect_applies && (c.refl[0] != 0.0 || c.refl[1] != 0.0 || c.refl[2] != 0.0)) {
             unsigned long long at = atomicAdd(next_count, 1ull);
             if ((int64_t)at < next_cap) {
-                QueuedRay q;
+                QueuedRay qo;
                 for (int k = 0; k < 3; ++k) {
-                    q.o[k] = c.over_point[k];
-                    q.d[k] = c.reflectv[k];
+                    qo.o[k] = c.over_point[k];
+                    qo.d[k] = c.reflectv[k];
                 }
-                q.key = base | ((code * 2) & 0xFFFull);
-                q.parent = (int32_t)node;
-                q.slot = 0;
-                next_q[at] = q;
+                qo.key = base | ((code * 2) & 0xFFFull);
+                qo.parent = (int32_t)node;
+                qo.slot = 0;
+                next_q[at] = qo;
             } else {
                 atomicOr(err, kErrQueueOverflow);
             }
@@ -185,15 +256,15 @@ __device__ void shade_prepare(const DevScene& S, const Batch& B, const Ray& r, c
         if (refract_applies && !tf_zero) {
             unsigned long long at = atomicAdd(next_count, 1ull);
             if ((int64_t)at < next_cap) {
-                QueuedRay q;
+                QueuedRay qo;
                 for (int k = 0; k < 3; ++k) {
-                    q.o[k] = c.under_point[k];
-                    q.d[k] = refr_dir[k];
+                    qo.o[k] = c.under_point[k];
+                    qo.d[k] = refr_dir[k];
                 }
-                q.key = base | ((code * 2 + 1) & 0xFFFull);
-                q.parent = (int32_t)node;
-                q.slot = 1;
-                next_q[at] = q;
+                qo.key = base | ((code * 2 + 1) & 0xFFFull);
+                qo.parent = (int32_t)node;
+                qo.slot = 1;
+                next_q[at] = qo;
             } else {
                 atomicOr(err, kErrQueueOverflow);
             }
@@ -205,66 +276,12 @@ __device__ void shade_prepare(const DevScene& S, const Batch& B, const Ray& r, c
     rec[node] = nr;
 }
 
-__global__ void __launch_bounds__(kBlock) k_primary(DevScene S, Batch B, NodeRec* __restrict__ rec,
-                                                    QueuedRay* __restrict__ next_q, int64_t next_cap,
-                                                    unsigned long long* next_count, unsigned long long* counters,
-                                                    unsigned* err) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B.num_samples) return;
-    const int64_t pix = B.pixel_begin + s / B.spp;
-    const int sub = (int)(s % B.spp);
-    const int64_t hs = S.cam.hsize;
-    const int64_t row = B.row_begin + (pix / hs) * B.row_stride;
-    const int64_t col = pix % hs;
-    const double* jit = S.sample_table + 2 * sub;  // sub = v * usteps + u (get_point_2d layout)
-    Ray r;
-    ray_for_pixel(S.cam, (double)col, (double)row, jit, r);
-    unsigned e = 0;
-    Hit h;
-    const uint64_t global_sample = (uint64_t)((row * hs + col) * B.spp + sub);
-    const uint64_t key = (global_sample << 12) | 1ull;
-    if (closest_hit(S, r, h, e)) {
-        shade_prepare(S, B, r, h, s, key, -1, 0, rec, next_q, next_cap, next_count, counters, err);
-    } else {
-        rec[s].material = -1;
-        rec[s].parent = -1;
-    }
-    if (e) atomicOr(err, e);
-}
-
-__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
-                                                   NodeRec* __restrict__ rec, QueuedRay* __restrict__ next_q,
-                                                   int64_t next_cap, unsigned long long* next_count,
-                                                   unsigned long long* counters, unsigned* err) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const QueuedRay qr = q[i];
-    Ray r;
-    for (int k = 0; k < 3; ++k) {
-        r.o[k] = qr.o[k];
-        r.d[k] = qr.d[k];
-    }
-    unsigned e = 0;
-    Hit h;
-    if (closest_hit(S, r, h, e)) {
-        shade_prepare(S, B, r, h, i, qr.key, qr.parent, qr.slot, rec, next_q, next_cap, next_count, counters, err);
-    } else {
-        NodeRec m;
-        m.material = -1;
-        m.parent = qr.parent;
-        m.slot = qr.slot;
-        rec[i].material = m.material;
-        rec[i].parent = m.parent;
-        rec[i].slot = m.slot;
-    }
-    if (e) atomicOr(err, e);
-}
-
 // one lane per (node, light sample j); lanes of a node are consecutive
-__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
-                                                   const int32_t* __restrict__ j_light,
-                                                   const int32_t* __restrict__ j_point, int32_t samples_per_node,
-                                                   int32_t* __restrict__ counts, unsigned* err) {
+template <int kFeat>
+__global__ void __launch_bounds__(kTraceBlock) k_shadow(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
+                                                        const int32_t* __restrict__ j_light,
+                                                        const int32_t* __restrict__ j_point, int32_t samples_per_node,
+                                                        int32_t* __restrict__ counts, unsigned* err) {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = tid < n * samples_per_node;
     int64_t node = 0;
@@ -289,7 +306,8 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, Batch B, const No
             r.o[2] = nr->over_point[2];
             normalize3(v, r.d);
             unsigned e = 0;
-            lit = !shadowed(S, r, distance, e);
+            double unused;
+            lit = walk<true, kFeat>(S, r, distance, unused, frt_walk_smem, e) == 0;
             if (e) atomicOr(err, e);
         }
     }
@@ -478,6 +496,7 @@ struct frt_scene_handle {
     int32_t* j_light = nullptr;
     int32_t* j_point = nullptr;
     int32_t samples_per_node = 0;
+    size_t lds_bytes = 0;  // dynamic LDS of the traversal kernels
     // work buffers (grow on demand)
     struct Level {
         frt::NodeRec* rec = nullptr;
@@ -488,6 +507,8 @@ struct frt_scene_handle {
         int64_t cap = 0;
     };
     std::vector<Level> levels;
+    frt::HitRec* hits = nullptr;  // closest hits of the level being traced
+    int64_t hits_cap = 0;
     double* sample_col = nullptr;
     int64_t sample_cap = 0;
     double* out_dev = nullptr;
@@ -584,9 +605,51 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     S.lights = upload(h, sc->lights, (size_t)sc->num_lights, rc);
     S.light_points = upload(h, sc->light_points, (size_t)sc->light_point_len, rc);
     S.sample_table = upload(h, sc->sample_table, (size_t)(2 * sc->camera.usteps * sc->camera.vsteps), rc);
+    {
+        // per node: does the leaf's material cast shadows (read by the shadow walk)
+        std::vector<uint8_t> casts((size_t)std::max(1, sc->num_nodes), 0);
+        for (int i = 0; i < sc->num_nodes; ++i) {
+            const int m = sc->nodes[i].material;
+            casts[(size_t)i] = (m >= 0 && m < sc->num_materials && sc->materials[m].casts_shadow) ? 1 : 0;
+        }
+        S.casts = upload(h, casts.data(), casts.size(), rc);
+    }
     if (rc) {
         frt_scene_release(h);
         return -1;
+    }
+    {
+        // per-lane walk capacities (see frt_traverse.hpp): exact bounds from the tree
+        static const int kMaxHits[10] = {4, 2, 4, 1, 1, 2, 4, 1, 0, 0};  // by frt_node_type
+        const int nn = sc->num_nodes;
+        std::vector<int> xf_cnt(nn, 0), comp_cnt(nn, 0), csg_top(nn, -1), list_need(nn, 0);
+        int xf_depth = 0, comp_depth = 0, list_cap = 0, features = 0;
+        for (int i = 0; i < nn; ++i) {
+            const frt_node& nd = sc->nodes[i];
+            const int par = nd.parent;
+            const bool composite = nd.type == FRT_GROUP || nd.type == FRT_CSG;
+            if (nd.type == FRT_CSG) features |= frt::kFeatCsg;
+            if (nd.type == FRT_TOROID) features |= frt::kFeatTorus;
+            csg_top[i] = par >= 0 && csg_top[par] >= 0 ? csg_top[par] : (nd.type == FRT_CSG ? i : -1);
+            xf_cnt[i] = (par >= 0 ? xf_cnt[par] : 0) + (composite && nd.xform >= 0 ? 1 : 0);
+            comp_cnt[i] = (par >= 0 && csg_top[par] >= 0 ? comp_cnt[par] : 0) + (composite && csg_top[i] >= 0 ? 1 : 0);
+            xf_depth = std::max(xf_depth, xf_cnt[i]);
+            comp_depth = std::max(comp_depth, comp_cnt[i]);
+            if (!composite && csg_top[i] >= 0 && nd.type >= 0 && nd.type < 10) {
+                list_need[csg_top[i]] += kMaxHits[nd.type];
+                list_cap = std::max(list_cap, list_need[csg_top[i]]);
+            }
+        }
+        S.list_cap = list_cap;
+        S.comp_depth = comp_depth;
+        S.xf_depth = xf_depth;
+        S.features = features;
+        h->lds_bytes = (size_t)frt::walk_lds_bytes_per_lane(list_cap, comp_depth, xf_depth) * frt::kTraceBlock;
+        if (h->lds_bytes > 64 * 1024) {
+            frt_scene_release(h);
+            return fail("frt_scene_upload: scene needs " + std::to_string(h->lds_bytes) +
+                        " B of LDS per traversal block (CSG lists / nesting too large)");
+        }
     }
     S.num_nodes = sc->num_nodes;
     S.num_roots = sc->num_roots;
@@ -632,6 +695,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(L.child));
         hip_ignore(hipFree(L.counts));
     }
+    hip_ignore(hipFree(h->hits));
     hip_ignore(hipFree(h->sample_col));
     hip_ignore(hipFree(h->out_dev));
     hip_ignore(hipFree(h->counters));
@@ -666,7 +730,7 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     return 0;
 }
 
-static inline unsigned grid_for(int64_t n) { return (unsigned)((n + frt::kBlock - 1) / frt::kBlock); }
+static inline unsigned grid_for(int64_t n, int block = frt::kBlock) { return (unsigned)((n + block - 1) / block); }
 
 // Kernel timing without host synchronisation: events are recorded around each
 // launch on the engine stream and read back once the frame has completed.
@@ -708,6 +772,43 @@ static void collect_timings(frt_scene_handle* h, frt_frame_stats* st) {
     h->ev_marks.clear();
     h->ev_used = 0;
 }
+
+}  // extern "C"
+
+// scene-specialised traversal kernels: the template instance without CSG
+// frames / the quartic keeps register pressure down for scenes that lack them
+template <int F>
+static void launch_trace_f(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n) {
+    hipLaunchKernelGGL(frt::k_trace<F>, dim3(grid_for(n, frt::kTraceBlock)), dim3(frt::kTraceBlock), h->lds_bytes,
+                       h->stream, h->S, B, q, n, h->hits, h->err);
+}
+
+static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n) {
+    switch (h->S.features & 3) {
+    case 0: launch_trace_f<0>(h, B, q, n); break;
+    case 1: launch_trace_f<1>(h, B, q, n); break;
+    case 2: launch_trace_f<2>(h, B, q, n); break;
+    default: launch_trace_f<3>(h, B, q, n); break;
+    }
+}
+
+template <int F>
+static void launch_shadow_f(frt_scene_handle* h, const frt::Batch& B, const frt::NodeRec* rec, int64_t n, int32_t* counts) {
+    const int64_t work = n * h->samples_per_node;
+    hipLaunchKernelGGL(frt::k_shadow<F>, dim3(grid_for(work, frt::kTraceBlock)), dim3(frt::kTraceBlock), h->lds_bytes,
+                       h->stream, h->S, B, rec, n, h->j_light, h->j_point, h->samples_per_node, counts, h->err);
+}
+
+static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::NodeRec* rec, int64_t n, int32_t* counts) {
+    switch (h->S.features & 3) {
+    case 0: launch_shadow_f<0>(h, B, rec, n, counts); break;
+    case 1: launch_shadow_f<1>(h, B, rec, n, counts); break;
+    case 2: launch_shadow_f<2>(h, B, rec, n, counts); break;
+    default: launch_shadow_f<3>(h, B, rec, n, counts); break;
+    }
+}
+
+extern "C" {
 
 static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
     using namespace frt;
@@ -758,22 +859,22 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
             auto& N = h->levels[d + 1];
             FRT_HIP(hipMemsetAsync(L.child, 0, (size_t)n * 24 * sizeof(double), h->stream));
             FRT_HIP(hipMemsetAsync(L.counts, 0, (size_t)n * std::max(1, h->S.num_lights) * sizeof(int32_t), h->stream));
+            if (grow(&h->hits, h->hits_cap, n)) return -1;
+            const QueuedRay* q = d == 0 ? nullptr : L.q;
             {
                 KTimer t(h, st, d == 0 ? 5 : 0);
-                if (d == 0) {
-                    hipLaunchKernelGGL(k_primary, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, N.q,
-                                       N.cap, h->counters + d + 1, h->counters + 16, h->err);
-                } else {
-                    hipLaunchKernelGGL(k_extend, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.q, n, L.rec,
-                                       N.q, N.cap, h->counters + d + 1, h->counters + 16, h->err);
-                }
+                launch_trace(h, B, q, n);
+                FRT_HIP(hipGetLastError());
+            }
+            {
+                KTimer t(h, st, 6);
+                hipLaunchKernelGGL(k_prepare, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
+                                   L.rec, N.q, N.cap, h->counters + d + 1, h->counters + 16, h->err);
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.include_direct && h->samples_per_node > 0) {
                 KTimer t(h, st, 1);
-                const int64_t work = n * h->samples_per_node;
-                hipLaunchKernelGGL(k_shadow, dim3(grid_for(work)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
-                                   h->j_light, h->j_point, h->samples_per_node, L.counts, h->err);
+                launch_shadow(h, B, L.rec, n, L.counts);
                 FRT_HIP(hipGetLastError());
             }
             {

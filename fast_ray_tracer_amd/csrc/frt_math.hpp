@@ -109,123 +109,153 @@ __device__ __forceinline__ void slab(double o, double d, double lo, double hi, d
     }
 }
 
-__device__ __forceinline__ bool box_hit(const double* bb, const Ray& r) {
+// bbox_intersect (bounding_box.c:164-177); also reports the entry / exit t
+__device__ __forceinline__ bool box_range(const double* bb, const Ray& r, double& tmin, double& tmax) {
     double x0, x1, y0, y1, z0, z1;
     slab(r.o[0], r.d[0], bb[0], bb[3], x0, x1);
     slab(r.o[1], r.d[1], bb[1], bb[4], y0, y1);
     slab(r.o[2], r.d[2], bb[2], bb[5], z0, z1);
-    return fmax(fmax(x0, y0), z0) <= fmin(fmin(x1, y1), z1);
+    tmin = fmax(fmax(x0, y0), z0);
+    tmax = fmin(fmin(x1, y1), z1);
+    return tmin <= tmax;
 }
+
+__device__ __forceinline__ bool box_hit(const double* bb, const Ray& r) {
+    double a, b;
+    return box_range(bb, r, a, b);
+}
+
+// ---- up to four values in registers: appended / read with constant-index
+// selects only, so no per-lane scratch array is ever materialised ----
+struct Vals4 {
+    double v0, v1, v2, v3;
+    int n;
+    __device__ __forceinline__ void push(double x) {
+        v0 = n == 0 ? x : v0;
+        v1 = n == 1 ? x : v1;
+        v2 = n == 2 ? x : v2;
+        v3 = n == 3 ? x : v3;
+        ++n;
+    }
+    __device__ __forceinline__ double at(int i) const { return i == 0 ? v0 : i == 1 ? v1 : i == 2 ? v2 : v3; }
+};
 
 // ---- quartic (reference Roots3And4.c:43-244) ----
 __device__ __forceinline__ bool is_zero(double x) { return x > -kEqnEps && x < kEqnEps; }
 
-__device__ inline int solve_quadric(double c0, double c1, double c2, double* s) {
+// SolveQuadric (Roots3And4.c:43-71): roots appended to R
+__device__ __forceinline__ void solve_quadric(double c0, double c1, double c2, Vals4& R) {
     double p = c1 / (2 * c2);
     double q = c0 / c2;
     double D = p * p - q;
     if (is_zero(D)) {
-        s[0] = -p;
-        return 1;
+        R.push(-p);
+        return;
     }
-    if (D < 0) return 0;
+    if (D < 0) return;
     double sd = sqrt(D);
-    s[0] = sd - p;
-    s[1] = -sd - p;
-    return 2;
+    R.push(sd - p);
+    R.push(-sd - p);
 }
 
-__device__ inline int solve_cubic(const double* c, double* s) {
-    double A = c[2] / c[3], B = c[1] / c[3], C = c[0] / c[3];
+// SolveCubic (Roots3And4.c:74-134) for c[3] = 1 callers: roots appended to R (R.n = 0 on entry)
+__device__ __forceinline__ void solve_cubic(double c0, double c1, double c2, double c3, Vals4& R) {
+    double A = c2 / c3, B = c1 / c3, C = c0 / c3;
     double sq_A = A * A;
     double p = 1.0 / 3 * (-1.0 / 3 * sq_A + B);
     double q = 1.0 / 2 * (2.0 / 27 * A * sq_A - 1.0 / 3 * A * B + C);
     double cb_p = p * p * p;
     double D = q * q + cb_p;
+    double s0, s1 = 0, s2 = 0;
     int num;
     if (is_zero(D)) {
         if (is_zero(q)) {
-            s[0] = 0;
+            s0 = 0;
             num = 1;
         } else {
             double u = cbrt(-q);
-            s[0] = 2 * u;
-            s[1] = -u;
+            s0 = 2 * u;
+            s1 = -u;
             num = 2;
         }
     } else if (D < 0) {
         double phi = 1.0 / 3 * acos(-q / sqrt(-cb_p));
         double t = 2 * sqrt(-p);
-        s[0] = t * cos(phi);
-        s[1] = -t * cos(phi + kPi / 3);
-        s[2] = -t * cos(phi - kPi / 3);
+        s0 = t * cos(phi);
+        s1 = -t * cos(phi + kPi / 3);
+        s2 = -t * cos(phi - kPi / 3);
         num = 3;
     } else {
         double sd = sqrt(D);
         double u = cbrt(sd - q);
         double v = -cbrt(sd + q);
-        s[0] = u + v;
+        s0 = u + v;
         num = 1;
     }
     double sub = 1.0 / 3 * A;
-    for (int i = 0; i < num; ++i) s[i] -= sub;
-    return num;
+    R.push(s0 - sub);
+    if (num > 1) R.push(s1 - sub);
+    if (num > 2) R.push(s2 - sub);
 }
 
-__device__ __noinline__ int solve_quartic(const double* c, double* s) {
-    double coeffs[4];
-    double A = c[3] / c[4], B = c[2] / c[4], C = c[1] / c[4], D = c[0] / c[4];
+// SolveQuartic (Roots3And4.c:137-244) with c[4] the leading coefficient
+__device__ __forceinline__ void solve_quartic(double c0, double c1, double c2, double c3, double c4, Vals4& R) {
+    R.n = 0;
+    double A = c3 / c4, B = c2 / c4, C = c1 / c4, D = c0 / c4;
     double sq_A = A * A;
     double p = -3.0 / 8 * sq_A + B;
     double q = 1.0 / 8 * sq_A * A - 1.0 / 2 * A * B + C;
     double r = -3.0 / 256 * sq_A * sq_A + 1.0 / 16 * sq_A * B - 1.0 / 4 * A * C + D;
-    int num;
     if (is_zero(r)) {
-        coeffs[0] = q;
-        coeffs[1] = p;
-        coeffs[2] = 0;
-        coeffs[3] = 1;
-        num = solve_cubic(coeffs, s);
-        s[num++] = 0;
+        solve_cubic(q, p, 0, 1, R);
+        R.push(0);
     } else {
-        coeffs[0] = 1.0 / 2 * r * p - 1.0 / 8 * q * q;
-        coeffs[1] = -r;
-        coeffs[2] = -1.0 / 2 * p;
-        coeffs[3] = 1;
-        (void)solve_cubic(coeffs, s);
-        double z = s[0];
+        Vals4 cub{0, 0, 0, 0, 0};
+        solve_cubic(1.0 / 2 * r * p - 1.0 / 8 * q * q, -r, -1.0 / 2 * p, 1, cub);
+        double z = cub.v0;
         double u = z * z - r;
         double v = 2 * z - p;
         if (is_zero(u)) u = 0;
         else if (u > 0) u = sqrt(u);
-        else return 0;
+        else return;
         if (is_zero(v)) v = 0;
         else if (v > 0) v = sqrt(v);
-        else return 0;
-        num = solve_quadric(z - u, q < 0 ? -v : v, 1, s);
-        num += solve_quadric(z + u, q < 0 ? v : -v, 1, s + num);
+        else return;
+        solve_quadric(z - u, q < 0 ? -v : v, 1, R);
+        solve_quadric(z + u, q < 0 ? v : -v, 1, R);
     }
     double sub = 1.0 / 4 * A;
-    for (int i = 0; i < num; ++i) s[i] -= sub;
-    return num;
+    R.v0 -= sub;  // unused slots are never read
+    R.v1 -= sub;
+    R.v2 -= sub;
+    R.v3 -= sub;
 }
 
-// ---- primitive intersections: hits appended in the reference's emission order ----
-// Returns the number of hits written to h (<= 4).
-__device__ __forceinline__ int leaf_hits(const frt_node& nd, int ni, const double* __restrict__ prim,
-                                         const Ray& r, Hit* h) {
+// ---- primitive intersections: hit t values appended in the reference's
+// emission order (H.n <= 4); triangles also report the hit's (u, v) ----
+struct LeafHits {
+    Vals4 t;
+    double u, v;
+};
+
+template <bool kTorus = true>
+__device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __restrict__ prim, const Ray& r,
+                                          LeafHits& H) {
+    H.t.n = 0;
+    H.t.v0 = H.t.v1 = H.t.v2 = H.t.v3 = 0.0;
     switch (nd.type) {
     case FRT_SPHERE: {  // sphere.c:14-39
         double a = dot3(r.d, r.d);
         double b = 2 * dot3(r.d, r.o);
         double c = dot3(r.o, r.o) - 1.0;
         double disc = b * b - 4 * a * c;
-        if (disc < 0) return 0;
+        if (disc < 0) return;
         disc = sqrt(disc);
         a = 1.0 / (2 * a);
-        h[0] = Hit{(-b - disc) * a, -1, -1, ni};
-        h[1] = Hit{(-b + disc) * a, -1, -1, ni};
-        return 2;
+        H.t.v0 = (-b - disc) * a;
+        H.t.v1 = (-b + disc) * a;
+        H.t.n = 2;
+        return;
     }
     case FRT_CUBE: {  // cube.c:56-77
         double x0, x1, y0, y1, z0, z1;
@@ -233,44 +263,48 @@ __device__ __forceinline__ int leaf_hits(const frt_node& nd, int ni, const doubl
         slab(r.o[1], r.d[1], -1, 1, y0, y1);
         slab(r.o[2], r.d[2], -1, 1, z0, z1);
         double tmin = fmax(fmax(x0, y0), z0), tmax = fmin(fmin(x1, y1), z1);
-        if (tmin > tmax) return 0;
-        h[0] = Hit{tmin, -1, -1, ni};
-        h[1] = Hit{tmax, -1, -1, ni};
-        return 2;
+        if (tmin > tmax) return;
+        H.t.v0 = tmin;
+        H.t.v1 = tmax;
+        H.t.n = 2;
+        return;
     }
     case FRT_PLANE:  // plane.c:11-24
-        if (fabs(r.d[1]) < kEps) return 0;
-        h[0] = Hit{-r.o[1] / r.d[1], -1, -1, ni};
-        return 1;
+        if (fabs(r.d[1]) < kEps) return;
+        H.t.v0 = -r.o[1] / r.d[1];
+        H.t.n = 1;
+        return;
     case FRT_TRIANGLE:
     case FRT_SMOOTH_TRIANGLE: {  // triangle.c:11-44
         const double* p = prim + nd.prim;
         double dce2[3], p1o[3], oce1[3];
         cross3(r.d, p + FRT_TRI_E2, dce2);
         double det = dot3(p + FRT_TRI_E1, dce2);
-        if (fabs(det) < kEps) return 0;
+        if (fabs(det) < kEps) return;
         double f = 1.0 / det;
         p1o[0] = r.o[0] - p[0];
         p1o[1] = r.o[1] - p[1];
         p1o[2] = r.o[2] - p[2];
         double u = f * dot3(p1o, dce2);
-        if (u < 0 || u > 1) return 0;
+        if (u < 0 || u > 1) return;
         cross3(p1o, p + FRT_TRI_E1, oce1);
         double v = f * dot3(r.d, oce1);
-        if (v < 0 || (u + v) > 1) return 0;
-        h[0] = Hit{f * dot3(p + FRT_TRI_E2, oce1), u, v, ni};
-        return 1;
+        if (v < 0 || (u + v) > 1) return;
+        H.t.v0 = f * dot3(p + FRT_TRI_E2, oce1);
+        H.t.n = 1;
+        H.u = u;
+        H.v = v;
+        return;
     }
     case FRT_CYLINDER: {  // cylinder.c:11-87
         const double* p = prim + nd.prim;
         double mn = p[0], mx = p[1];
-        int n = 0;
         double a = r.d[0] * r.d[0] + r.d[2] * r.d[2];
         double b = 2 * (r.o[0] * r.d[0] + r.o[2] * r.d[2]);
         double c = r.o[0] * r.o[0] + r.o[2] * r.o[2] - 1;
         if (!feq(a, 0.0)) {
             double disc = b * b - 4 * a * c;
-            if (disc < 0) return 0;
+            if (disc < 0) return;
             double sq = sqrt(disc);
             double t0 = (-b - sq) / (2 * a), t1 = (-b + sq) / (2 * a);
             if (t0 > t1) {
@@ -279,31 +313,30 @@ __device__ __forceinline__ int leaf_hits(const frt_node& nd, int ni, const doubl
                 t1 = tt;
             }
             double y0 = r.o[1] + t0 * r.d[1];
-            if (mn <= y0 && y0 <= mx) h[n++] = Hit{t0, -1, -1, ni};
+            if (mn <= y0 && y0 <= mx) H.t.push(t0);
             double y1 = r.o[1] + t1 * r.d[1];
-            if (mn <= y1 && y1 <= mx) h[n++] = Hit{t1, -1, -1, ni};
+            if (mn <= y1 && y1 <= mx) H.t.push(t1);
         }
-        if (p[2] == 0.0 || feq(r.d[1], 0.0)) return n;
+        if (p[2] == 0.0 || feq(r.d[1], 0.0)) return;
         double ta = (mn - r.o[1]) / r.d[1];
         double tb = (mx - r.o[1]) / r.d[1];
         double xa = r.o[0] + ta * r.d[0], za = r.o[2] + ta * r.d[2];
-        if (xa * xa + za * za <= 1) h[n++] = Hit{ta, -1, -1, ni};
+        if (xa * xa + za * za <= 1) H.t.push(ta);
         double xb = r.o[0] + tb * r.d[0], zb = r.o[2] + tb * r.d[2];
-        if (xb * xb + zb * zb <= 1) h[n++] = Hit{tb, -1, -1, ni};
-        return n;
+        if (xb * xb + zb * zb <= 1) H.t.push(tb);
+        return;
     }
     case FRT_CONE: {  // cone.c:11-96
         const double* p = prim + nd.prim;
         double mn = p[0], mx = p[1];
-        int n = 0;
         double a = r.d[0] * r.d[0] + r.d[2] * r.d[2] - r.d[1] * r.d[1];
         double b = 2 * (r.o[0] * r.d[0] + r.o[2] * r.d[2] - r.o[1] * r.d[1]);
         double c = r.o[0] * r.o[0] + r.o[2] * r.o[2] - r.o[1] * r.o[1];
         if (feq(a, 0.0)) {
-            if (!feq(b, 0.0)) h[n++] = Hit{-c / (2 * b), -1, -1, ni};
+            if (!feq(b, 0.0)) H.t.push(-c / (2 * b));
         } else {
             double disc = b * b - 4 * a * c;
-            if (disc < 0) return 0;
+            if (disc < 0) return;
             double sq = sqrt(disc);
             double t0 = (-b - sq) / (2 * a), t1 = (-b + sq) / (2 * a);
             if (t0 > t1) {
@@ -312,20 +345,21 @@ __device__ __forceinline__ int leaf_hits(const frt_node& nd, int ni, const doubl
                 t1 = tt;
             }
             double y0 = r.o[1] + t0 * r.d[1];
-            if (mn < y0 && y0 < mx) h[n++] = Hit{t0, -1, -1, ni};
+            if (mn < y0 && y0 < mx) H.t.push(t0);
             double y1 = r.o[1] + t1 * r.d[1];
-            if (mn < y1 && y1 < mx) h[n++] = Hit{t1, -1, -1, ni};
+            if (mn < y1 && y1 < mx) H.t.push(t1);
         }
-        if (p[2] == 0.0 || feq(r.d[1], 0.0)) return n;
+        if (p[2] == 0.0 || feq(r.d[1], 0.0)) return;
         double ta = (mn - r.o[1]) / r.d[1];
         double xa = r.o[0] + ta * r.d[0], za = r.o[2] + ta * r.d[2];
-        if (xa * xa + za * za <= fabs(mn)) h[n++] = Hit{ta, -1, -1, ni};
+        if (xa * xa + za * za <= fabs(mn)) H.t.push(ta);
         double tb = (mx - r.o[1]) / r.d[1];
         double xb = r.o[0] + tb * r.d[0], zb = r.o[2] + tb * r.d[2];
-        if (xb * xb + zb * zb <= fabs(mx)) h[n++] = Hit{tb, -1, -1, ni};
-        return n;
+        if (xb * xb + zb * zb <= fabs(mx)) H.t.push(tb);
+        return;
     }
     case FRT_TOROID: {  // toroid.c:15-52
+        if constexpr (!kTorus) return;
         const double* p = prim + nd.prim;
         double r1 = p[0], r2 = p[1];
         double ox = r.o[0], oy = r.o[1], oz = r.o[2];
@@ -334,16 +368,21 @@ __device__ __forceinline__ int leaf_hits(const frt_node& nd, int ni, const doubl
         double e = ox * ox + oy * oy + oz * oz - r1 * r1 - r2 * r2;
         double f = ox * dx + oy * dy + oz * dz;
         double four_a_sq = 4.0 * r1 * r1;
-        double coeffs[5] = {e * e - four_a_sq * (r2 * r2 - oy * oy), 4.0 * f * e + 2.0 * four_a_sq * oy * dy,
-                            2.0 * sum_d_sq * e + 4.0 * f * f + four_a_sq * dy * dy, 4.0 * sum_d_sq * f,
-                            sum_d_sq * sum_d_sq};
-        double sol[4];
-        int n = solve_quartic(coeffs, sol);
-        for (int k = 0; k < n; ++k) h[k] = Hit{sol[n - 1 - k], -1, -1, ni};
-        return n;
+        Vals4 sol;
+        solve_quartic(e * e - four_a_sq * (r2 * r2 - oy * oy), 4.0 * f * e + 2.0 * four_a_sq * oy * dy,
+                      2.0 * sum_d_sq * e + 4.0 * f * f + four_a_sq * dy * dy, 4.0 * sum_d_sq * f,
+                      sum_d_sq * sum_d_sq, sol);
+        // the reference appends the roots last to first
+        const int n = sol.n;
+        H.t.v0 = sol.at(n - 1);
+        H.t.v1 = sol.at(n - 2);
+        H.t.v2 = sol.at(n - 3);
+        H.t.v3 = sol.at(n - 4);
+        H.t.n = n;
+        return;
     }
     default:
-        return 0;
+        return;
     }
 }
 

@@ -437,7 +437,17 @@ __device__ inline void normal_at(const DevScene& S, int leaf, const double* wp, 
     normalize3(ln, n);
 }
 
-__device__ inline void prepare(const DevScene& S, const Ray& r, const Hit& h, Comps& c) {
+__device__ inline void prepare(const DevScene& S, const Ray& r, Hit h, Comps& c) {
+    if (S.nodes[h.node].type == FRT_TRIANGLE || S.nodes[h.node].type == FRT_SMOOTH_TRIANGLE) {
+        // the walk keeps (t, node) only; the triangle's (u, v) are recomputed with the same ray
+        LeafHits H;
+        const Ray lr = leaf_local_ray(S, h.node, r);
+        leaf_hits<false>(S.nodes[h.node], S.prim, lr, H);
+        if (H.t.n > 0) {
+            h.u = H.u;
+            h.v = H.v;
+        }
+    }
     c.leaf = h.node;
     c.material = S.nodes[h.node].material;
     for (int k = 0; k < 3; ++k) c.p[k] = r.o[k] + r.d[k] * h.t;

@@ -36,7 +36,7 @@ class FrameStats(ctypes.Structure):
                 ("shadow_kernel_bytes", ctypes.c_double)]
 
     def as_dict(self) -> dict:
-        names = ["extend", "shadow", "shade", "combine", "resolve", "primary", "k6", "k7"]
+        names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "k7"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),

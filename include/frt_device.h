@@ -189,7 +189,7 @@ typedef struct frt_frame_stats {
     uint64_t hits;                /* path nodes shaded */
     uint64_t errors;              /* capacity / depth overflows (non-zero = result invalid) */
     double render_ms;             /* wall time of the device work (events) */
-    double kernel_ms[8];          /* per-kernel accumulated time: extend, shadow, shade, combine, resolve, gen */
+    double kernel_ms[8];          /* per-kernel accumulated time: trace, shadow, shade, combine, resolve, trace (level 0), prepare */
     uint64_t kernel_launches[8];
     double shadow_kernel_bytes;   /* algorithmic bytes moved by the shadow kernel (DESIGN.md byte model) */
 } frt_frame_stats;
