@@ -131,23 +131,26 @@ extern __shared__ __align__(16) char frt_walk_smem[];
 template <int kFeat>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
                                                        HitRec* __restrict__ hits, unsigned* err) {
+    // every lane of the wave takes part in the (wave-coherent) walk
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Ray r;
-    if (q == nullptr) {
-        uint64_t key;
-        camera_ray(S, B, i, r, key);
-    } else {
-        const QueuedRay& qr = q[i];
-        for (int k = 0; k < 3; ++k) {
-            r.o[k] = qr.o[k];
-            r.d[k] = qr.d[k];
+    const bool live = i < n;
+    Ray r{{0, 0, 0}, {0, 0, 1}};
+    if (live) {
+        if (q == nullptr) {
+            uint64_t key;
+            camera_ray(S, B, i, r, key);
+        } else {
+            const QueuedRay& qr = q[i];
+            for (int k = 0; k < 3; ++k) {
+                r.o[k] = qr.o[k];
+                r.d[k] = qr.d[k];
+            }
         }
     }
     unsigned e = 0;
     double t;
-    const int node = walk<false, kFeat>(S, r, 0.0, t, frt_walk_smem, e);
-    hits[i] = HitRec{t, node, 0};
+    const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e);
+    if (live) hits[i] = HitRec{t, node, 0};
     if (e) atomicOr(err, e);
 }
 
@@ -286,7 +289,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow(DevScene S, Batch B, con
     const bool valid = tid < n * samples_per_node;
     int64_t node = 0;
     int light = 0;
-    bool lit = false;
+    bool live = false;
+    Ray r{{0, 0, 0}, {0, 0, 1}};
+    double distance = 0.0;
     if (valid) {
         node = tid / samples_per_node;
         const int j = (int)(tid % samples_per_node);
@@ -294,23 +299,24 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow(DevScene S, Batch B, con
         const int pt = j_point[j];
         const NodeRec* nr = rec + node;
         if (nr->material >= 0) {
+            live = true;
             const frt_light& L = S.lights[light];
             const int row = light_row(L, B.seed, nr->key, light, 0);
             const double* lp = S.light_points + L.points + 3 * ((int64_t)row * L.num_samples + pt);
             // is_shadowed (renderer.c:74-93)
             double v[3] = {lp[0] - nr->over_point[0], lp[1] - nr->over_point[1], lp[2] - nr->over_point[2]};
-            double distance = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-            Ray r;
+            distance = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
             r.o[0] = nr->over_point[0];
             r.o[1] = nr->over_point[1];
             r.o[2] = nr->over_point[2];
             normalize3(v, r.d);
-            unsigned e = 0;
-            double unused;
-            lit = walk<true, kFeat>(S, r, distance, unused, frt_walk_smem, e) == 0;
-            if (e) atomicOr(err, e);
         }
     }
+    // every lane of the wave takes part in the (wave-coherent) walk
+    unsigned e = 0;
+    double unused;
+    const bool lit = walk<true, kFeat>(S, r, distance, live, unused, frt_walk_smem, e) == 0 && live;
+    if (e) atomicOr(err, e);
     // segmented wave reduction: lanes with the same (node, light) are contiguous
     const int lane = threadIdx.x & 63;
     const int64_t key = valid ? node * S.num_lights + light : -1 - (int64_t)lane;
@@ -644,7 +650,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         S.comp_depth = comp_depth;
         S.xf_depth = xf_depth;
         S.features = features;
-        h->lds_bytes = (size_t)frt::walk_lds_bytes_per_lane(list_cap, comp_depth, xf_depth) * frt::kTraceBlock;
+        h->lds_bytes = (size_t)frt::walk_lds_bytes(list_cap, comp_depth, xf_depth);
         if (h->lds_bytes > 64 * 1024) {
             frt_scene_release(h);
             return fail("frt_scene_upload: scene needs " + std::to_string(h->lds_bytes) +

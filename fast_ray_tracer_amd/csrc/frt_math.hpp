@@ -92,8 +92,14 @@ __device__ __forceinline__ Ray xf_ray(const double* m, const Ray& r) {
 __device__ __forceinline__ void slab(double o, double d, double lo, double hi, double& a, double& b) {
     double nl = lo - o, nh = hi - o, t0, t1;
     if (fabs(d) >= kEps) {
+#ifdef FRT_EXPERIMENT_FASTDIV
+        const double rd = __builtin_amdgcn_rcp(d);
+        t0 = nl * rd;
+        t1 = nh * rd;
+#else
         t0 = nl / d;
         t1 = nh / d;
+#endif
     } else {
         t0 = nl * __builtin_inf();
         if (isnan(t0)) t0 = nl < 0 ? -__builtin_inf() : __builtin_inf();

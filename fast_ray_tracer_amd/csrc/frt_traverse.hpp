@@ -71,36 +71,47 @@ enum ErrBits : unsigned {
 
 __device__ __forceinline__ const double* xform_of(const DevScene& S, int x) { return S.xforms + 16 * (size_t)x; }
 
-// bytes of dynamic LDS per lane for a scene's capacities (host and device agree)
-__host__ __device__ constexpr int walk_lds_bytes_per_lane(int list_cap, int comp_depth, int xf_depth) {
-    return 12 * list_cap + 12 * comp_depth + 4 * xf_depth;
-}
-
-// per-lane views into the dynamic LDS of a traversal block
+// Dynamic LDS of a traversal block. Per lane ([k * kTraceBlock + lane]):
+// the CSG list (t, node) and each open composite's list start / mid. Per wave
+// (uniform, [wave * depth + k]): the node of each open composite frame and of
+// each open transform frame.
 struct WalkLds {
-    double* lt;  // list t          [k * kTraceBlock]
-    int* ln;     // list node
-    int* cn;     // composite frame: node
-    int* cs;     // composite frame: list start
-    int* ca;     // composite frame: CSG mid / group current-child start
-    int* xn;     // transform frame: node
+    double* lt;  // list t          (per lane)
+    int* ln;     // list node       (per lane)
+    int* cs;     // composite frame: list start (per lane)
+    int* ca;     // composite frame: CSG mid / group current-child start (per lane)
+    int* cn;     // composite frame: node (per wave)
+    int* xn;     // transform frame: node (per wave)
     __device__ __forceinline__ double& T(int k) const { return lt[k * kTraceBlock]; }
     __device__ __forceinline__ int& N(int k) const { return ln[k * kTraceBlock]; }
 };
 
+__host__ __device__ constexpr int walk_lds_bytes(int list_cap, int comp_depth, int xf_depth) {
+    return (12 * list_cap + 8 * comp_depth) * kTraceBlock + 4 * (comp_depth + xf_depth) * (kTraceBlock / 64);
+}
+
 __device__ __forceinline__ WalkLds walk_lds(const DevScene& S, char* smem) {
-    const int l = threadIdx.x;
-    const int L = S.list_cap, C = S.comp_depth;
-    WalkLds w;
+    const int l = threadIdx.x, w = threadIdx.x >> 6;
+    const int L = S.list_cap, C = S.comp_depth, X = S.xf_depth;
+    WalkLds v;
     double* lt = (double*)smem;
     int* ints = (int*)(lt + L * kTraceBlock);
-    w.lt = lt + l;
-    w.ln = ints + l;
-    w.cn = ints + L * kTraceBlock + l;
-    w.cs = w.cn + C * kTraceBlock;
-    w.ca = w.cs + C * kTraceBlock;
-    w.xn = w.ca + C * kTraceBlock;
-    return w;
+    v.lt = lt + l;
+    v.ln = ints + l;
+    v.cs = ints + L * kTraceBlock + l;
+    v.ca = v.cs + C * kTraceBlock;
+    int* wave = ints + (L + 2 * C) * kTraceBlock;
+    v.cn = wave + w * C;
+    v.xn = wave + (kTraceBlock / 64) * C + w * X;
+    return v;
+}
+
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+    return uniform(x);
 }
 
 __device__ __forceinline__ void sort_range(const WalkLds& W, int b, int e) {
@@ -145,14 +156,15 @@ __device__ __forceinline__ int csg_filter(const WalkLds& W, int op, int left_beg
     return to;
 }
 
-// close the composite at frame top: group -> sort; CSG -> csg_local_intersect's tail. Returns the new list end.
-__device__ __forceinline__ int close_composite(const DevScene& S, const WalkLds& W, int node, int start, int aux, int n) {
-    const frt_node& nd = S.nodes[node];
+// close a composite: group -> sort (group.c:144); CSG -> csg_local_intersect's tail (csg.c:93-121).
+// Returns the lane's new list end.
+__device__ __forceinline__ int close_composite(const frt_node& nd, int node, const WalkLds& W, int start, int mid,
+                                               int n) {
     if (nd.type == FRT_GROUP) {
         sort_range(W, start, n);
         return n;
     }
-    const int mid = aux, right = nd.right, op = nd.prim;
+    const int right = nd.right, op = nd.prim;
     if (n == start) return start;
     if (mid == start) return csg_filter(W, op, node + 1, right, mid, n, start);  // left empty: right list as is
     if (n == mid) return csg_filter(W, op, node + 1, right, start, mid, start);  // right empty
@@ -160,130 +172,150 @@ __device__ __forceinline__ int close_composite(const DevScene& S, const WalkLds&
     return csg_filter(W, op, node + 1, right, start, n, start);
 }
 
-// rebuild the current ray from the world ray through the open transform frames
-__device__ __forceinline__ void rebuild_ray(const DevScene& S, const WalkLds& W, int sp, const Ray& world, Ray& cur) {
-    cur = world;
-    for (int k = 0; k < sp; ++k) cur = xf_ray(xform_of(S, S.nodes[W.xn[k * kTraceBlock]].xform), cur);
-}
-
 __device__ __forceinline__ bool behind(double tmax) { return tmax < -1e-6 * (1.0 + fabs(tmax)); }
 
-// One walk for both ray kinds.
+constexpr int kDone = 0x7fffffff;  // resume index of a lane whose walk has finished
+
+// One wave-coherent walk for both ray kinds. The wave visits the pre-order
+// nodes together (node index, frames and box / leaf decisions of the wave
+// are uniform, so node records and transforms come in through scalar loads);
+// each lane carries its own ray, result and `resume` index: a lane whose ray
+// misses a composite's box (or that has finished) sits out until the walk
+// reaches `resume`. A composite is entered if any lane enters it; when no lane
+// is active the walk jumps to the smallest resume index.
 //   kShadow = false: returns the closest-hit leaf (-1 = miss), its t in best_t.
 //   kShadow = true:  returns 1 if shadowed (is_shadowed), else 0.
+// Lanes that should not trace pass live = false (they still take part).
 template <bool kShadow, int kFeat>
-__device__ int walk(const DevScene& S, const Ray& world, double distance, double& best_t, char* smem, unsigned& err) {
+__device__ int walk(const DevScene& S, const Ray& world, double distance, bool live, double& best_t, char* smem,
+                    unsigned& err) {
     constexpr bool kCsg = (kFeat & kFeatCsg) != 0;
     constexpr bool kTorus = (kFeat & kFeatTorus) != 0;
     const WalkLds W = walk_lds(S, smem);
     int best = -1;
+    int result = 0;
     best_t = 0.0;
     for (int ri = 0; ri < S.num_roots; ++ri) {
+        if (__ballot(live) == 0) break;
         const int root = S.roots[ri];
         const int end = S.nodes[root].skip;
         const bool may_skip_behind = !kShadow || ri == S.num_roots - 1;
-        int sp = 0;  // open transform frames
-        int cp = 0;  // open composite frames (inside a CSG unit)
-        int n = 0;   // list entries of the open CSG unit
+        int sp = 0;  // open transform frames (uniform)
+        int cp = 0;  // open composite frames inside a CSG unit (uniform)
+        int n = 0;   // list entries of the open CSG unit (per lane)
+        int resume = live ? 0 : kDone;
         bool any_entry = false;
         Ray cur = world;
         int i = root;
         while (true) {
-            // ---- close what the walk has left ----
+            // ---- close the composites the walk has left ----
             if constexpr (kCsg) {
-                bool unit_done = false;
                 while (cp > 0) {
-                    const int top = W.cn[(cp - 1) * kTraceBlock];
+                    const int top = uniform(W.cn[cp - 1]);
                     const frt_node& tn = S.nodes[top];
                     if (i < tn.skip) {
-                        // group_local_intersect's stop rule for a group inside the unit
-                        if (kShadow && tn.type == FRT_GROUP && i > top + 1) {
+                        // group_local_intersect's stop rule (group.c:114-121) for a group inside the unit
+                        if (kShadow && tn.type == FRT_GROUP && i > top + 1 && i >= resume) {
                             bool go_on = true;
                             for (int k = W.ca[(cp - 1) * kTraceBlock]; go_on && k < n; ++k) go_on = W.T(k) <= 0;
-                            if (!go_on) {
-                                i = tn.skip;
-                                continue;
-                            }
+                            if (!go_on) resume = tn.skip;
                         }
                         break;
                     }
-                    n = close_composite(S, W, top, W.cs[(cp - 1) * kTraceBlock], W.ca[(cp - 1) * kTraceBlock], n);
+                    n = close_composite(tn, top, W, W.cs[(cp - 1) * kTraceBlock], W.ca[(cp - 1) * kTraceBlock], n);
                     --cp;
-                    unit_done = cp == 0;
-                }
-                if (unit_done) {
-                    // a CSG unit of the main walk is complete: its list is [0, n)
-                    if (!kShadow) {
-                        for (int k = 0; k < n; ++k) {
-                            const double t = W.T(k);
-                            if (t > 0 && (best < 0 || t < best_t)) {
-                                best_t = t;
-                                best = W.N(k);
+                    if (cp == 0) {
+                        // a CSG unit of the main walk is complete: the lane's list is [0, n)
+                        if (resume != kDone) {
+                            if (!kShadow) {
+                                for (int k = 0; k < n; ++k) {
+                                    const double t = W.T(k);
+                                    if (t > 0 && (best < 0 || t < best_t)) {
+                                        best_t = t;
+                                        best = W.N(k);
+                                    }
+                                }
+                            } else if (n > 0) {
+                                any_entry = true;
+                                bool stop_here = false;
+                                for (int k = 0; k < n; ++k) stop_here = stop_here || !(W.T(k) <= 0);
+                                if (stop_here) {
+                                    bool blocked = false;
+                                    for (int k = 0; k < n; ++k) {
+                                        const double t = W.T(k);
+                                        blocked = blocked || (t > 0 && t < distance && S.casts[W.N(k)]);
+                                    }
+                                    result = blocked ? 1 : 0;
+                                    resume = kDone;
+                                }
                             }
                         }
-                    } else if (n > 0) {
-                        any_entry = true;
-                        bool stop_here = false;
-                        for (int k = 0; k < n; ++k) stop_here = stop_here || !(W.T(k) <= 0);
-                        if (stop_here) {
-                            for (int k = 0; k < n; ++k) {
-                                const double t = W.T(k);
-                                if (t > 0 && t < distance && S.casts[W.N(k)]) return 1;
-                            }
-                            return 0;
-                        }
+                        n = 0;
                     }
-                    n = 0;
                 }
             }
-            if (sp > 0 && i >= S.nodes[W.xn[(sp - 1) * kTraceBlock]].skip) {
+            // ---- pop transform frames, rebuild the ray from the world ray ----
+            if (sp > 0 && i >= S.nodes[uniform(W.xn[sp - 1])].skip) {
                 do {
                     --sp;
-                } while (sp > 0 && i >= S.nodes[W.xn[(sp - 1) * kTraceBlock]].skip);
-                rebuild_ray(S, W, sp, world, cur);
+                } while (sp > 0 && i >= S.nodes[uniform(W.xn[sp - 1])].skip);
+                cur = world;
+                for (int k = 0; k < sp; ++k) cur = xf_ray(xform_of(S, S.nodes[uniform(W.xn[k])].xform), cur);
             }
             if (i >= end) break;
+            const bool active = i >= resume;
+            if (__ballot(active) == 0) {
+                // every inactive lane has resume > i; max() only guards progress
+                i = min(end, max(wave_min(resume), i + 1));
+                continue;
+            }
             if constexpr (kCsg) {
                 if (cp > 0) {
-                    const int top = W.cn[(cp - 1) * kTraceBlock];
+                    const int top = uniform(W.cn[cp - 1]);
                     const frt_node& tn = S.nodes[top];
                     if (tn.type == FRT_GROUP || i == tn.right) W.ca[(cp - 1) * kTraceBlock] = n;
                 }
             }
-            // ---- visit node i ----
+            // ---- visit node i (uniform) ----
             const frt_node& nd = S.nodes[i];
             const int type = nd.type;
             const int xf = nd.xform;
             const Ray lr = xf >= 0 ? xf_ray(xform_of(S, xf), cur) : cur;
             if (type == FRT_GROUP || type == FRT_CSG) {
-                double tmin, tmax;
-                bool enter = box_range(nd.bbox, lr, tmin, tmax);
-                if (cp == 0) {  // skips that cannot change this walk's answer (see header)
-                    if (may_skip_behind && behind(tmax)) enter = false;
-                    if (!kShadow && best >= 0 && tmin > best_t + 1e-6 * (1.0 + fabs(best_t))) enter = false;
+                bool enter = false;
+                if (active) {
+                    double tmin, tmax;
+                    enter = box_range(nd.bbox, lr, tmin, tmax);
+                    if (cp == 0) {  // skips that cannot change this lane's answer (see header)
+                        if (may_skip_behind && behind(tmax)) enter = false;
+                        if (!kShadow && best >= 0 && tmin > best_t + 1e-6 * (1.0 + fabs(best_t))) enter = false;
+                    }
+                    if (!enter) resume = nd.skip;
                 }
-                if (!enter) {
+                if (__ballot(enter) == 0) {
                     i = nd.skip;
                     continue;
                 }
                 if (xf >= 0) {
-                    if (sp >= S.xf_depth) {
+                    if (sp >= S.xf_depth) {  // cannot happen: xf_depth is exact (upload)
                         err |= kErrXformDepth;
+                        resume = kDone;
                         i = nd.skip;
                         continue;
                     }
-                    W.xn[sp * kTraceBlock] = i;
+                    if ((threadIdx.x & 63) == 0) W.xn[sp] = i;
                     ++sp;
                     cur = lr;
                 }
                 if constexpr (kCsg) {
                     if (type == FRT_CSG || cp > 0) {
-                        if (cp >= S.comp_depth) {
+                        if (cp >= S.comp_depth) {  // cannot happen: comp_depth is exact (upload)
                             err |= kErrCsgDepth;
+                            resume = kDone;
                             i = nd.skip;
                             continue;
                         }
-                        W.cn[cp * kTraceBlock] = i;
+                        if ((threadIdx.x & 63) == 0) W.cn[cp] = i;
                         W.cs[cp * kTraceBlock] = n;
                         W.ca[cp * kTraceBlock] = n;
                         ++cp;
@@ -292,49 +324,55 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, double
                 ++i;
                 continue;
             }
-            LeafHits H;
-            leaf_hits<kTorus>(nd, S.prim, lr, H);
-            if (kCsg && cp > 0) {
+            if (active) {
+                LeafHits H;
+                leaf_hits<kTorus>(nd, S.prim, lr, H);
+                if (kCsg && cp > 0) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (j < H.t.n) {
-                        if (n < S.list_cap) {
-                            W.T(n) = H.t.at(j);
-                            W.N(n) = i;
-                            ++n;
-                        } else {
-                            err |= kErrCsgOverflow;
+                    for (int j = 0; j < 4; ++j) {
+                        if (j < H.t.n) {
+                            if (n < S.list_cap) {
+                                W.T(n) = H.t.at(j);
+                                W.N(n) = i;
+                                ++n;
+                            } else {
+                                err |= kErrCsgOverflow;
+                            }
                         }
                     }
-                }
-            } else if (!kShadow) {
+                } else if (!kShadow) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const double t = H.t.at(j);
-                    if (j < H.t.n && t > 0 && (best < 0 || t < best_t)) {
-                        best_t = t;
-                        best = i;
+                    for (int j = 0; j < 4; ++j) {
+                        const double t = H.t.at(j);
+                        if (j < H.t.n && t > 0 && (best < 0 || t < best_t)) {
+                            best_t = t;
+                            best = i;
+                        }
+                    }
+                } else if (H.t.n > 0) {
+                    any_entry = true;
+                    bool stop_here = false;
+                    bool blocked = false;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const double t = H.t.at(j);
+                        if (j < H.t.n) {
+                            stop_here = stop_here || !(t <= 0);
+                            blocked = blocked || (t > 0 && t < distance);
+                        }
+                    }
+                    if (stop_here) {
+                        result = blocked && S.casts[i] ? 1 : 0;
+                        resume = kDone;
                     }
                 }
-            } else if (H.t.n > 0) {
-                any_entry = true;
-                bool stop_here = false;
-                bool blocked = false;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const double t = H.t.at(j);
-                    if (j < H.t.n) {
-                        stop_here = stop_here || !(t <= 0);
-                        blocked = blocked || (t > 0 && t < distance);
-                    }
-                }
-                if (stop_here) return blocked && S.casts[i];
             }
             ++i;
         }
-        if (kShadow && any_entry) return 0;  // intersect_world(stop) ends after the first shape with entries
+        if (kShadow && live && resume != kDone && any_entry) live = false;  // first world shape with entries ends it
+        if (resume == kDone) live = false;
     }
-    return kShadow ? 0 : best;
+    return kShadow ? result : best;
 }
 
 // recompute a leaf's local ray (through every transformed ancestor, root first,
