@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -280,8 +281,13 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
 }
 
 // one lane per (node, light sample j); lanes of a node are consecutive
+#ifdef FRT_SHADOW_WAVES
+#define FRT_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(FRT_SHADOW_WAVES, 8)))
+#else
+#define FRT_SHADOW_ATTR
+#endif
 template <int kFeat>
-__global__ void __launch_bounds__(kTraceBlock) k_shadow(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
+__global__ void __launch_bounds__(kTraceBlock) FRT_SHADOW_ATTR k_shadow(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
                                                         const int32_t* __restrict__ j_light,
                                                         const int32_t* __restrict__ j_point, int32_t samples_per_node,
                                                         int32_t* __restrict__ counts, unsigned* err) {
@@ -315,7 +321,11 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow(DevScene S, Batch B, con
     // every lane of the wave takes part in the (wave-coherent) walk
     unsigned e = 0;
     double unused;
+#ifdef FRT_EXPERIMENT_NOWALK
+    const bool lit = live && distance > 0.5;
+#else
     const bool lit = walk<true, kFeat>(S, r, distance, live, unused, frt_walk_smem, e) == 0 && live;
+#endif
     if (e) atomicOr(err, e);
     // segmented wave reduction: lanes with the same (node, light) are contiguous
     const int lane = threadIdx.x & 63;
@@ -625,6 +635,102 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         return -1;
     }
     {
+        // walk visit records (frt_traverse.hpp WalkNode)
+        auto invert4 = [](const double* m, double* out) -> bool {  // Gauss-Jordan, partial pivoting
+            double a[4][8];
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 8; ++c) a[r][c] = c < 4 ? m[4 * r + c] : (c - 4 == r ? 1.0 : 0.0);
+            for (int c = 0; c < 4; ++c) {
+                int p = c;
+                for (int r = c + 1; r < 4; ++r)
+                    if (std::fabs(a[r][c]) > std::fabs(a[p][c])) p = r;
+                if (a[p][c] == 0.0) return false;
+                for (int k = 0; k < 8; ++k) std::swap(a[c][k], a[p][k]);
+                const double inv = 1.0 / a[c][c];
+                for (int k = 0; k < 8; ++k) a[c][k] *= inv;
+                for (int r = 0; r < 4; ++r)
+                    if (r != c) {
+                        const double f = a[r][c];
+                        for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
+                    }
+            }
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) out[4 * r + c] = a[r][4 + c];
+            return true;
+        };
+        std::vector<frt::WalkNode> wn((size_t)std::max(1, sc->num_nodes));
+        for (int i = 0; i < sc->num_nodes; ++i) {
+            const frt_node& nd = sc->nodes[i];
+            frt::WalkNode& w = wn[(size_t)i];
+            std::memset(&w, 0, sizeof(w));
+            w.type = nd.type;
+            w.skip = nd.skip;
+            w.right = nd.right;
+            w.op = nd.type == FRT_CSG ? nd.prim : 0;
+            w.prim = nd.type == FRT_CSG || nd.type == FRT_GROUP ? 0 : nd.prim;
+            w.has_xf = nd.xform >= 0 ? 1 : 0;
+            const int m = nd.material;
+            w.casts = (m >= 0 && m < sc->num_materials && sc->materials[m].casts_shadow) ? 1 : 0;
+            for (int k = 0; k < 6; ++k) w.bbox[k] = nd.bbox[k];
+            const double* mi = nd.xform >= 0 ? sc->xforms + 16 * (size_t)nd.xform : nullptr;
+            if (mi)
+                for (int k = 0; k < 12; ++k) w.m[k] = mi[k];
+            for (int r = 0; r < 3; ++r) {
+                w.mrow_l1[r] = 0.f;
+                for (int c = 0; c < 3; ++c) {
+                    const double v = mi ? mi[4 * r + c] : (r == c ? 1.0 : 0.0);
+                    w.mrow[3 * r + c] = (float)v;
+                    w.mrow_l1[r] += (float)std::fabs(v);
+                }
+                w.mrow_l1[r] *= 1.0001f;
+            }
+            // prefilter bound in the parent frame (frt_traverse.hpp): cubes, spheres and transformed composites
+            const bool composite = nd.type == FRT_GROUP || nd.type == FRT_CSG;
+            const bool want = nd.type == FRT_CUBE || nd.type == FRT_SPHERE || (composite && mi);
+            double fwd[16];
+            bool ok = want && (!mi || invert4(mi, fwd));
+            double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+            if (ok && nd.type == FRT_SPHERE) {
+                for (int a = 0; a < 3; ++a) {
+                    const double c = mi ? fwd[4 * a + 3] : 0.0;
+                    const double e = mi ? std::sqrt(fwd[4 * a] * fwd[4 * a] + fwd[4 * a + 1] * fwd[4 * a + 1] +
+                                                    fwd[4 * a + 2] * fwd[4 * a + 2])
+                                        : 1.0;
+                    lo[a] = c - e;
+                    hi[a] = c + e;
+                }
+            } else if (ok) {
+                const double bl[3] = {composite ? nd.bbox[0] : -1.0, composite ? nd.bbox[1] : -1.0,
+                                      composite ? nd.bbox[2] : -1.0};
+                const double bh[3] = {composite ? nd.bbox[3] : 1.0, composite ? nd.bbox[4] : 1.0,
+                                      composite ? nd.bbox[5] : 1.0};
+                for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(bl[a]) && std::isfinite(bh[a]);
+                for (int c = 0; ok && c < 8; ++c) {
+                    const double p[3] = {(c & 1) ? bh[0] : bl[0], (c & 2) ? bh[1] : bl[1], (c & 4) ? bh[2] : bl[2]};
+                    for (int a = 0; a < 3; ++a) {
+                        const double v = mi ? fwd[4 * a] * p[0] + fwd[4 * a + 1] * p[1] + fwd[4 * a + 2] * p[2] +
+                                                  fwd[4 * a + 3]
+                                            : p[a];
+                        lo[a] = std::min(lo[a], v);
+                        hi[a] = std::max(hi[a], v);
+                    }
+                }
+            }
+            for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(lo[a]) && std::isfinite(hi[a]);
+            if (ok) {
+                for (int a = 0; a < 3; ++a) {
+                    const double pad = 1e-7 * ((hi[a] - lo[a]) + std::max(std::fabs(lo[a]), std::fabs(hi[a]))) + 1e-12;
+                    w.pbox[a] = lo[a] - pad;
+                    w.pbox[a + 3] = hi[a] + pad;
+                }
+                w.pre = 1 | (nd.type == FRT_SPHERE ? 0 : 2);
+            } else {
+                w.pre = 0;
+            }
+        }
+        S.wn = upload(h, wn.data(), wn.size(), rc);
+    }
+    {
         // per-lane walk capacities (see frt_traverse.hpp): exact bounds from the tree
         static const int kMaxHits[10] = {4, 2, 4, 1, 1, 2, 4, 1, 0, 0};  // by frt_node_type
         const int nn = sc->num_nodes;
@@ -657,6 +763,10 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                         " B of LDS per traversal block (CSG lists / nesting too large)");
         }
     }
+    {
+        const char* wf = std::getenv("FRT_WALK_FLAGS");  // A/B experiments only
+        S.walk_flags = wf ? std::atoi(wf) : 0;
+    }
     S.num_nodes = sc->num_nodes;
     S.num_roots = sc->num_roots;
     S.num_lights = sc->num_lights;
@@ -679,6 +789,13 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             return -1;
         }
     }
+#ifdef FRT_WALK_STATS
+    if (hipMalloc((void**)&h->S.dbg, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(h->S.dbg, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        frt_scene_release(h);
+        return fail("frt_scene_upload: debug counters");
+    }
+#endif
     if (hipStreamCreate(&h->stream) != hipSuccess || hipMalloc((void**)&h->counters, 32 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&h->err, sizeof(unsigned)) != hipSuccess || hipEventCreate(&h->ev[0]) != hipSuccess ||
         hipEventCreate(&h->ev[1]) != hipSuccess) {
@@ -816,6 +933,21 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::N
 
 extern "C" {
 
+#ifdef FRT_WALK_STATS
+// debug builds: dump the walk counters accumulated so far to stderr
+static void dump_walk_stats(frt_scene_handle* h) {
+    unsigned long long c[16];
+    if (hipMemcpy(c, h->S.dbg, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) return;
+    const char* names[8] = {"composite_visits", "leaf_visits", "active_lane_visits", "jumps", "walks", "live_lanes",
+                            "prefilter_rejects", "lanes_tested"};
+    for (int k = 0; k < 2; ++k) {
+        std::fprintf(stderr, "walk stats (%s):", k == 0 ? "shadow" : "closest");
+        for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %s=%llu", names[j], c[8 * k + j]);
+        std::fprintf(stderr, "\n");
+    }
+}
+#endif
+
 static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
     using namespace frt;
     FRT_HIP(hipSetDevice(h->device));
@@ -936,6 +1068,9 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         st->errors = err;
         collect_timings(h, st);
     }
+#ifdef FRT_WALK_STATS
+    dump_walk_stats(h);
+#endif
     if (err) {
         char buf[128];
         std::snprintf(buf, sizeof(buf), "render: device error bits 0x%x", err);

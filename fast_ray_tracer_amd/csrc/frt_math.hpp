@@ -81,6 +81,19 @@ __device__ __forceinline__ void xf_normal_t(const double* m, const double* n, do
     r[2] = z;
 }
 
+// ray transform of the traversal: drops the m[i3] * 0.0 terms of the direction,
+// which can only flip the sign of a zero component; the walk's only uses of
+// direction components are |d| < EPSILON guards, products and sums, none of
+// which can see that sign in a t value or a hit / miss decision
+__device__ __forceinline__ Ray xf_ray_walk(const double* m, const Ray& r) {
+    Ray t;
+    xf_point(m, r.o, t.o);
+    t.d[0] = (m[0] * r.d[0] + m[1] * r.d[1]) + m[2] * r.d[2];
+    t.d[1] = (m[4] * r.d[0] + m[5] * r.d[1]) + m[6] * r.d[2];
+    t.d[2] = (m[8] * r.d[0] + m[9] * r.d[1]) + m[10] * r.d[2];
+    return t;
+}
+
 __device__ __forceinline__ Ray xf_ray(const double* m, const Ray& r) {
     Ray t;
     xf_point(m, r.o, t.o);
@@ -89,30 +102,24 @@ __device__ __forceinline__ Ray xf_ray(const double* m, const Ray& r) {
 }
 
 // check_axis / bbox_check_axis (cube.c:16-53, bounding_box.c:124-162)
+// max / min of slab values, which are never NaN (finite quotients or the +-inf
+// of the EPSILON branch): fmax / fmin as in the reference, one v_max_f64 /
+// v_min_f64 each (arithmetic results need no IEEE-mode canonicalisation)
+__device__ __forceinline__ double max2(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ double min2(double a, double b) { return __builtin_fmin(a, b); }
+
+// check_axis / bbox_check_axis (cube.c:16-53, bounding_box.c:124-162), branch-free:
+// for |d| < EPSILON the reference takes n * INFINITY with NaN (n == 0) mapped to
+// (n < 0 ? -inf : inf) — i.e. exactly (n < 0 ? -inf : inf) for every n
 __device__ __forceinline__ void slab(double o, double d, double lo, double hi, double& a, double& b) {
-    double nl = lo - o, nh = hi - o, t0, t1;
-    if (fabs(d) >= kEps) {
-#ifdef FRT_EXPERIMENT_FASTDIV
-        const double rd = __builtin_amdgcn_rcp(d);
-        t0 = nl * rd;
-        t1 = nh * rd;
-#else
-        t0 = nl / d;
-        t1 = nh / d;
-#endif
-    } else {
-        t0 = nl * __builtin_inf();
-        if (isnan(t0)) t0 = nl < 0 ? -__builtin_inf() : __builtin_inf();
-        t1 = nh * __builtin_inf();
-        if (isnan(t1)) t1 = nh < 0 ? -__builtin_inf() : __builtin_inf();
+    const double nl = lo - o, nh = hi - o;
+    double t0 = nl / d, t1 = nh / d;
+    if (!(fabs(d) >= kEps)) {
+        t0 = nl < 0 ? -__builtin_inf() : __builtin_inf();
+        t1 = nh < 0 ? -__builtin_inf() : __builtin_inf();
     }
-    if (t0 > t1) {
-        a = t1;
-        b = t0;
-    } else {
-        a = t0;
-        b = t1;
-    }
+    a = min2(t0, t1);  // the reference's "if (t0 > t1) swap" for NaN-free values
+    b = max2(t0, t1);
 }
 
 // bbox_intersect (bounding_box.c:164-177); also reports the entry / exit t
@@ -121,9 +128,95 @@ __device__ __forceinline__ bool box_range(const double* bb, const Ray& r, double
     slab(r.o[0], r.d[0], bb[0], bb[3], x0, x1);
     slab(r.o[1], r.d[1], bb[1], bb[4], y0, y1);
     slab(r.o[2], r.d[2], bb[2], bb[5], z0, z1);
-    tmin = fmax(fmax(x0, y0), z0);
-    tmax = fmin(fmin(x1, y1), z1);
+    tmin = max2(max2(x0, y0), z0);
+    tmax = min2(min2(x1, y1), z1);
     return tmin <= tmax;
+}
+
+// ---- filtered box tests (decisions only; no IEEE division on the fast path) ----
+// v_rcp_f64 is good to ~2^-24 (tools/microbench/rcp_accuracy.hip); each Newton
+// step squares the error: one step <= 2^-48, two steps correctly rounded on 4M samples.
+template <int kSteps>
+__device__ __forceinline__ double recip(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+    return r;
+}
+
+__device__ __forceinline__ double finite_abs(double x) { return __builtin_isinf(x) ? 0.0 : fabs(x); }
+
+constexpr double kFilterRel = 0x1p-40;  // decision margin; the approximations are good to 2^-47
+
+// The reference's box decision (bounding_box_intersects, bounding_box.c:164-175),
+// exactly: slab t values from an approximate reciprocal (rc[a] ~ 1/d[a], one
+// Newton step), the |d| < EPSILON branch exact as in slab(); the comparison is
+// trusted when it clears a margin far above the approximation error, otherwise
+// the IEEE-division box_range() decides. tmin / tmax return the approximate values.
+__device__ __forceinline__ bool box_decide(const double* bb, const Ray& r, const double* rc, double& tmin,
+                                           double& tmax) {
+    double lo3[3], hi3[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double nl = bb[a] - r.o[a], nh = bb[a + 3] - r.o[a];
+        double t0 = nl * rc[a], t1 = nh * rc[a];
+        if (!(fabs(r.d[a]) >= kEps)) {
+            t0 = nl < 0 ? -__builtin_inf() : __builtin_inf();
+            t1 = nh < 0 ? -__builtin_inf() : __builtin_inf();
+        }
+        lo3[a] = min2(t0, t1);
+        hi3[a] = max2(t0, t1);
+    }
+    tmin = max2(max2(lo3[0], lo3[1]), lo3[2]);
+    tmax = min2(min2(hi3[0], hi3[1]), hi3[2]);
+    const double margin = kFilterRel * (finite_abs(tmin) + finite_abs(tmax));
+    if (tmin <= tmax - margin) return true;
+    if (tmin > tmax + margin) return false;
+    double a, b;
+    return box_range(bb, r, a, b);
+}
+
+// Conservative line-vs-box test for the prefilter: false only when the exact
+// line misses bb (an inflated parent-space bound of a node) by far more than
+// the approximation error. Direction components below 1e-200 count as parallel.
+__device__ __forceinline__ bool box_may_hit(const double* bb, const Ray& r, const double* rc, double& tmin,
+                                            double& tmax) {
+    double lo3[3], hi3[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double nl = bb[a] - r.o[a], nh = bb[a + 3] - r.o[a];
+        double t0 = nl * rc[a], t1 = nh * rc[a];
+        if (!(fabs(r.d[a]) >= 1e-200)) {  // parallel: inside the slab iff nl <= 0 <= nh
+            t0 = nl <= 0 ? -__builtin_inf() : __builtin_inf();
+            t1 = nh >= 0 ? __builtin_inf() : -__builtin_inf();
+        }
+        lo3[a] = min2(t0, t1);
+        hi3[a] = max2(t0, t1);
+    }
+    tmin = max2(max2(lo3[0], lo3[1]), lo3[2]);
+    tmax = min2(min2(hi3[0], hi3[1]), hi3[2]);
+    return !(tmin > tmax + kFilterRel * (finite_abs(tmin) + finite_abs(tmax)));
+}
+
+// origin strictly inside the box: every slab gives t0 < 0 < t1 (signs of IEEE
+// quotients are exact; the EPSILON branch gives -inf / +inf), so the reference's
+// box test reports a hit with tmin < 0 < tmax — decided without any slab arithmetic
+__device__ __forceinline__ bool origin_inside(const double* bb, const Ray& r) {
+    return bb[0] < r.o[0] && r.o[0] < bb[3] && bb[1] < r.o[1] && r.o[1] < bb[4] && bb[2] < r.o[2] && r.o[2] < bb[5];
+}
+
+// Could a local direction component (row a of the node's inverse transform
+// applied to the parent-frame direction) fall below EPSILON, where the
+// reference's slab test switches to its infinite-slab branch? Float estimate
+// with an error bound: rows / L1 norms from the upload, df = float(d), dmax = max |df|.
+__device__ __forceinline__ bool quirk_possible(const float* mrow, const float* l1, const float* df, float dmax) {
+    bool q = false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float v = (mrow[3 * a] * df[0] + mrow[3 * a + 1] * df[1]) + mrow[3 * a + 2] * df[2];
+        q = q || fabsf(v) < 1.0001e-5f + 0x1p-19f * l1[a] * dmax;
+    }
+    return q;
 }
 
 __device__ __forceinline__ bool box_hit(const double* bb, const Ray& r) {
@@ -244,12 +337,12 @@ struct LeafHits {
     double u, v;
 };
 
+// type: enum frt_node_type; p: the leaf's parameters in prim_data
 template <bool kTorus = true>
-__device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __restrict__ prim, const Ray& r,
-                                          LeafHits& H) {
+__device__ __forceinline__ void leaf_hits(int type, const double* __restrict__ p, const Ray& r, LeafHits& H) {
     H.t.n = 0;
     H.t.v0 = H.t.v1 = H.t.v2 = H.t.v3 = 0.0;
-    switch (nd.type) {
+    switch (type) {
     case FRT_SPHERE: {  // sphere.c:14-39
         double a = dot3(r.d, r.d);
         double b = 2 * dot3(r.d, r.o);
@@ -268,7 +361,7 @@ __device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __re
         slab(r.o[0], r.d[0], -1, 1, x0, x1);
         slab(r.o[1], r.d[1], -1, 1, y0, y1);
         slab(r.o[2], r.d[2], -1, 1, z0, z1);
-        double tmin = fmax(fmax(x0, y0), z0), tmax = fmin(fmin(x1, y1), z1);
+        double tmin = max2(max2(x0, y0), z0), tmax = min2(min2(x1, y1), z1);
         if (tmin > tmax) return;
         H.t.v0 = tmin;
         H.t.v1 = tmax;
@@ -282,7 +375,6 @@ __device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __re
         return;
     case FRT_TRIANGLE:
     case FRT_SMOOTH_TRIANGLE: {  // triangle.c:11-44
-        const double* p = prim + nd.prim;
         double dce2[3], p1o[3], oce1[3];
         cross3(r.d, p + FRT_TRI_E2, dce2);
         double det = dot3(p + FRT_TRI_E1, dce2);
@@ -303,7 +395,6 @@ __device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __re
         return;
     }
     case FRT_CYLINDER: {  // cylinder.c:11-87
-        const double* p = prim + nd.prim;
         double mn = p[0], mx = p[1];
         double a = r.d[0] * r.d[0] + r.d[2] * r.d[2];
         double b = 2 * (r.o[0] * r.d[0] + r.o[2] * r.d[2]);
@@ -333,7 +424,6 @@ __device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __re
         return;
     }
     case FRT_CONE: {  // cone.c:11-96
-        const double* p = prim + nd.prim;
         double mn = p[0], mx = p[1];
         double a = r.d[0] * r.d[0] + r.d[2] * r.d[2] - r.d[1] * r.d[1];
         double b = 2 * (r.o[0] * r.d[0] + r.o[2] * r.d[2] - r.o[1] * r.d[1]);
@@ -366,7 +456,6 @@ __device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __re
     }
     case FRT_TOROID: {  // toroid.c:15-52
         if constexpr (!kTorus) return;
-        const double* p = prim + nd.prim;
         double r1 = p[0], r2 = p[1];
         double ox = r.o[0], oy = r.o[1], oz = r.o[2];
         double dx = r.d[0], dy = r.d[1], dz = r.d[2];
@@ -389,6 +478,43 @@ __device__ __forceinline__ void leaf_hits(const frt_node& nd, const double* __re
     }
     default:
         return;
+    }
+}
+
+// Cube entries for a shadow-ray decision (cube.c:56-77 + the stop / blocked
+// tests of the caller): slab quotients from a one-Newton-step reciprocal
+// instead of IEEE divisions. The approximate (tmin, tmax) are returned only
+// when every comparison the caller makes with them — tmin <= tmax, t <= 0,
+// t < distance — clears a margin far above their error, so the decisions are
+// the exact ones; otherwise the exact cube test runs.
+__device__ __forceinline__ void cube_hits_for_decisions(const Ray& r, double distance, LeafHits& H) {
+    double lo3[3], hi3[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double nl = -1.0 - r.o[a], nh = 1.0 - r.o[a];
+        const double rc = recip<1>(r.d[a]);
+        double t0 = nl * rc, t1 = nh * rc;
+        if (!(fabs(r.d[a]) >= kEps)) {
+            t0 = nl < 0 ? -__builtin_inf() : __builtin_inf();
+            t1 = nh < 0 ? -__builtin_inf() : __builtin_inf();
+        }
+        lo3[a] = min2(t0, t1);
+        hi3[a] = max2(t0, t1);
+    }
+    const double tmin = max2(max2(lo3[0], lo3[1]), lo3[2]);
+    const double tmax = min2(min2(hi3[0], hi3[1]), hi3[2]);
+    const double m = kFilterRel * (finite_abs(tmin) + finite_abs(tmax) + distance);
+    const bool entries = tmin <= tmax;
+    bool robust = fabs(tmin - tmax) > m;
+    if (entries)
+        robust = robust && fabs(tmin) > m && fabs(tmax) > m && fabs(tmin - distance) > m && fabs(tmax - distance) > m;
+    H.t.v2 = H.t.v3 = 0.0;
+    if (robust) {
+        H.t.n = entries ? 2 : 0;
+        H.t.v0 = tmin;
+        H.t.v1 = tmax;
+    } else {
+        leaf_hits<false>(FRT_CUBE, nullptr, r, H);
     }
 }
 

@@ -442,7 +442,7 @@ __device__ inline void prepare(const DevScene& S, const Ray& r, Hit h, Comps& c)
         // the walk keeps (t, node) only; the triangle's (u, v) are recomputed with the same ray
         LeafHits H;
         const Ray lr = leaf_local_ray(S, h.node, r);
-        leaf_hits<false>(S.nodes[h.node], S.prim, lr, H);
+        leaf_hits<false>(S.nodes[h.node].type, S.prim + S.nodes[h.node].prim, lr, H);
         if (H.t.n > 0) {
             h.u = H.u;
             h.v = H.v;

@@ -34,7 +34,39 @@
 
 namespace frt {
 
+// Device visit record of one node for the walk (built at upload): everything a
+// visit reads sits in one 176-byte record, fetched with independent scalar loads
+// once the (wave-uniform) node index is known — no node -> transform chain.
+struct alignas(16) WalkNode {
+    int32_t type, skip, right, op;     // op: CSG operation
+    int32_t has_xf, casts, prim;       // prim: offset of the leaf's parameters in prim_data
+    int32_t pre;                       // bit0: pbox prefilter applies, bit1: check the EPSILON quirk first
+    double bbox[6];                    // composites: own-space bounds
+    double m[12];                      // inverse transform, rows 0-2 (has_xf)
+    double pbox[6];                    // prefilter: inflated bound of the node in its parent's frame
+    float mrow[9];                     // rows of m's 3x3 part (identity without transform), as float
+    float mrow_l1[3];                  // their L1 norms
+};
+
+// per-frame cache of the current ray: reciprocal direction (two Newton steps),
+// float direction and its largest magnitude (prefilter / quirk check)
+struct FrameCache {
+    double rc[3];
+    float df[3];
+    float dmax;
+};
+
+__device__ __forceinline__ void frame_cache(const Ray& r, FrameCache& c) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        c.rc[a] = recip<2>(r.d[a]);
+        c.df[a] = (float)r.d[a];
+    }
+    c.dmax = fmaxf(fmaxf(fabsf(c.df[0]), fabsf(c.df[1])), fabsf(c.df[2]));
+}
+
 struct DevScene {
+    const WalkNode* __restrict__ wn;
     const frt_node* __restrict__ nodes;
     const int32_t* __restrict__ roots;
     const double* __restrict__ xforms;
@@ -53,6 +85,8 @@ struct DevScene {
     int32_t comp_depth;  // open composites inside a CSG unit
     int32_t xf_depth;    // open transformed composites
     int32_t features;    // FeatureBits present in the scene
+    unsigned long long* dbg;  // walk statistics (FRT_WALK_STATS builds only)
+    int32_t walk_flags;       // FRT_WALK_FLAGS (A/B experiments): bit0 no prefilter, bit1 exact box decisions, bit2 exact cubes
     frt_camera cam;
     frt_config cfg;
 };
@@ -60,6 +94,10 @@ struct DevScene {
 enum FeatureBits : int { kFeatCsg = 1, kFeatTorus = 2 };
 
 constexpr int kTraceBlock = 128;  // lanes per block of the traversal kernels
+
+#ifndef FRT_PREFILTER
+#define FRT_PREFILTER 0  // parent-frame bound prefilter for leaves (costs registers; off by default)
+#endif
 
 enum ErrBits : unsigned {
     kErrCsgOverflow = 1u,
@@ -158,13 +196,12 @@ __device__ __forceinline__ int csg_filter(const WalkLds& W, int op, int left_beg
 
 // close a composite: group -> sort (group.c:144); CSG -> csg_local_intersect's tail (csg.c:93-121).
 // Returns the lane's new list end.
-__device__ __forceinline__ int close_composite(const frt_node& nd, int node, const WalkLds& W, int start, int mid,
-                                               int n) {
-    if (nd.type == FRT_GROUP) {
+__device__ __forceinline__ int close_composite(int type, int node, int right, int op, const WalkLds& W, int start,
+                                               int mid, int n) {
+    if (type == FRT_GROUP) {
         sort_range(W, start, n);
         return n;
     }
-    const int right = nd.right, op = nd.prim;
     if (n == start) return start;
     if (mid == start) return csg_filter(W, op, node + 1, right, mid, n, start);  // left empty: right list as is
     if (n == mid) return csg_filter(W, op, node + 1, right, start, mid, start);  // right empty
@@ -191,112 +228,183 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                     unsigned& err) {
     constexpr bool kCsg = (kFeat & kFeatCsg) != 0;
     constexpr bool kTorus = (kFeat & kFeatTorus) != 0;
+    constexpr int kNone = 0x7fffffff;
     const WalkLds W = walk_lds(S, smem);
     int best = -1;
     int result = 0;
     best_t = 0.0;
+#ifdef FRT_WALK_STATS
+    {
+        const unsigned long long lv = __ballot(live);
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+            atomicAdd(S.dbg + (kShadow ? 0 : 8) + 4, 1ull);
+            atomicAdd(S.dbg + (kShadow ? 0 : 8) + 5, (unsigned long long)__popcll(lv));
+        }
+    }
+#endif
     for (int ri = 0; ri < S.num_roots; ++ri) {
         if (__ballot(live) == 0) break;
         const int root = S.roots[ri];
-        const int end = S.nodes[root].skip;
+        const int end = S.wn[root].skip;
         const bool may_skip_behind = !kShadow || ri == S.num_roots - 1;
-        int sp = 0;  // open transform frames (uniform)
-        int cp = 0;  // open composite frames inside a CSG unit (uniform)
-        int n = 0;   // list entries of the open CSG unit (per lane)
+        // uniform walk state; the tops of both frame stacks are cached here
+        int sp = 0, xf_end = kNone;                             // transform frames
+        int cp = 0, c_node = 0, c_skip = kNone, c_right = 0;   // composite frames (inside a CSG unit)
+        int c_type = 0, c_op = 0;
+        int n = 0;  // list entries of the open CSG unit (per lane)
         int resume = live ? 0 : kDone;
         bool any_entry = false;
         Ray cur = world;
+#if FRT_PREFILTER
+        FrameCache fc;
+        frame_cache(cur, fc);
+#endif
         int i = root;
         while (true) {
             // ---- close the composites the walk has left ----
             if constexpr (kCsg) {
                 while (cp > 0) {
-                    const int top = uniform(W.cn[cp - 1]);
-                    const frt_node& tn = S.nodes[top];
-                    if (i < tn.skip) {
+                    if (i < c_skip) {
                         // group_local_intersect's stop rule (group.c:114-121) for a group inside the unit
-                        if (kShadow && tn.type == FRT_GROUP && i > top + 1 && i >= resume) {
+                        if (kShadow && c_type == FRT_GROUP && i > c_node + 1 && i >= resume) {
                             bool go_on = true;
                             for (int k = W.ca[(cp - 1) * kTraceBlock]; go_on && k < n; ++k) go_on = W.T(k) <= 0;
-                            if (!go_on) resume = tn.skip;
+                            if (!go_on) resume = c_skip;
                         }
                         break;
                     }
-                    n = close_composite(tn, top, W, W.cs[(cp - 1) * kTraceBlock], W.ca[(cp - 1) * kTraceBlock], n);
+                    n = close_composite(c_type, c_node, c_right, c_op, W, W.cs[(cp - 1) * kTraceBlock],
+                                        W.ca[(cp - 1) * kTraceBlock], n);
                     --cp;
-                    if (cp == 0) {
-                        // a CSG unit of the main walk is complete: the lane's list is [0, n)
-                        if (resume != kDone) {
-                            if (!kShadow) {
-                                for (int k = 0; k < n; ++k) {
-                                    const double t = W.T(k);
-                                    if (t > 0 && (best < 0 || t < best_t)) {
-                                        best_t = t;
-                                        best = W.N(k);
-                                    }
-                                }
-                            } else if (n > 0) {
-                                any_entry = true;
-                                bool stop_here = false;
-                                for (int k = 0; k < n; ++k) stop_here = stop_here || !(W.T(k) <= 0);
-                                if (stop_here) {
-                                    bool blocked = false;
-                                    for (int k = 0; k < n; ++k) {
-                                        const double t = W.T(k);
-                                        blocked = blocked || (t > 0 && t < distance && S.casts[W.N(k)]);
-                                    }
-                                    result = blocked ? 1 : 0;
-                                    resume = kDone;
+                    if (cp > 0) {
+                        c_node = uniform(W.cn[cp - 1]);
+                        const WalkNode& tn = S.wn[c_node];
+                        c_skip = tn.skip;
+                        c_right = tn.right;
+                        c_type = tn.type;
+                        c_op = tn.op;
+                        continue;
+                    }
+                    c_skip = kNone;
+                    // a CSG unit of the main walk is complete: the lane's list is [0, n)
+                    if (resume != kDone) {
+                        if (!kShadow) {
+                            for (int k = 0; k < n; ++k) {
+                                const double t = W.T(k);
+                                if (t > 0 && (best < 0 || t < best_t)) {
+                                    best_t = t;
+                                    best = W.N(k);
                                 }
                             }
+                        } else if (n > 0) {
+                            any_entry = true;
+                            bool stop_here = false;
+                            for (int k = 0; k < n; ++k) stop_here = stop_here || !(W.T(k) <= 0);
+                            if (stop_here) {
+                                bool blocked = false;
+                                for (int k = 0; k < n; ++k) {
+                                    const double t = W.T(k);
+                                    blocked = blocked || (t > 0 && t < distance && S.casts[W.N(k)]);
+                                }
+                                result = blocked ? 1 : 0;
+                                resume = kDone;
+                            }
                         }
-                        n = 0;
                     }
+                    n = 0;
                 }
             }
             // ---- pop transform frames, rebuild the ray from the world ray ----
-            if (sp > 0 && i >= S.nodes[uniform(W.xn[sp - 1])].skip) {
+            if (i >= xf_end) {
                 do {
                     --sp;
-                } while (sp > 0 && i >= S.nodes[uniform(W.xn[sp - 1])].skip);
+                    xf_end = sp > 0 ? S.wn[uniform(W.xn[sp - 1])].skip : kNone;
+                } while (i >= xf_end);
                 cur = world;
-                for (int k = 0; k < sp; ++k) cur = xf_ray(xform_of(S, S.nodes[uniform(W.xn[k])].xform), cur);
+                for (int k = 0; k < sp; ++k) cur = xf_ray_walk(S.wn[uniform(W.xn[k])].m, cur);
+#if FRT_PREFILTER
+                frame_cache(cur, fc);
+#endif
             }
             if (i >= end) break;
             const bool active = i >= resume;
             if (__ballot(active) == 0) {
+#ifdef FRT_WALK_STATS
+                if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(S.dbg + (kShadow ? 0 : 8) + 3, 1ull);
+#endif
                 // every inactive lane has resume > i; max() only guards progress
                 i = min(end, max(wave_min(resume), i + 1));
                 continue;
             }
             if constexpr (kCsg) {
-                if (cp > 0) {
-                    const int top = uniform(W.cn[cp - 1]);
-                    const frt_node& tn = S.nodes[top];
-                    if (tn.type == FRT_GROUP || i == tn.right) W.ca[(cp - 1) * kTraceBlock] = n;
-                }
+                if (cp > 0 && (c_type == FRT_GROUP || i == c_right)) W.ca[(cp - 1) * kTraceBlock] = n;
             }
             // ---- visit node i (uniform) ----
-            const frt_node& nd = S.nodes[i];
+            const WalkNode& nd = S.wn[i];
             const int type = nd.type;
-            const int xf = nd.xform;
-            const Ray lr = xf >= 0 ? xf_ray(xform_of(S, xf), cur) : cur;
+#ifdef FRT_WALK_STATS
+            {
+                const unsigned long long av = __ballot(active);
+                if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+                    atomicAdd(S.dbg + (kShadow ? 0 : 8) + ((type == FRT_GROUP || type == FRT_CSG) ? 0 : 1), 1ull);
+                    atomicAdd(S.dbg + (kShadow ? 0 : 8) + 2, (unsigned long long)__popcll(av));
+                }
+            }
+#endif
+            // prefilter: a lane whose ray cannot meet the node's parent-frame bound
+            // (and cannot take the EPSILON branch in its local test) skips the node
+            // A leaf of the main walk (outside CSG units) whose bound lies wholly
+            // behind the ray, or (closest hit) beyond the best t, has no entry
+            // that could matter either.
+            bool may = active;
+#if FRT_PREFILTER
+            if ((nd.pre & 1) && !(S.walk_flags & 1)) {
+                if (may) {
+                    double pt0, pt1;
+                    may = box_may_hit(nd.pbox, cur, fc.rc, pt0, pt1);
+                    if (may && cp == 0 && type != FRT_GROUP && type != FRT_CSG) {
+                        if (may_skip_behind && behind(pt1)) may = false;
+                        if (!kShadow && best >= 0 && pt0 > best_t + 1e-6 * (1.0 + fabs(best_t))) may = false;
+                    }
+                    if (!may && (nd.pre & 2)) may = quirk_possible(nd.mrow, nd.mrow_l1, fc.df, fc.dmax);
+                }
+            }
+#endif
+#ifdef FRT_WALK_STATS
+            {
+                const unsigned long long pv = __ballot(active && !may), fv = __ballot(may);
+                if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+                    atomicAdd(S.dbg + (kShadow ? 0 : 8) + 6, (unsigned long long)__popcll(pv));
+                    atomicAdd(S.dbg + (kShadow ? 0 : 8) + 7, (unsigned long long)__popcll(fv));
+                }
+            }
+#endif
             if (type == FRT_GROUP || type == FRT_CSG) {
                 bool enter = false;
-                if (active) {
-                    double tmin, tmax;
-                    enter = box_range(nd.bbox, lr, tmin, tmax);
+                if (may) {
+                    const Ray lr = nd.has_xf ? xf_ray_walk(nd.m, cur) : cur;
+                    double tmin = -1.0, tmax = 1.0;
+                    if (origin_inside(nd.bbox, lr)) {
+                        enter = true;
+                    } else if (S.walk_flags & 2) {
+                        enter = box_range(nd.bbox, lr, tmin, tmax);
+                    } else {
+                        double lrc[3];
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) lrc[a] = recip<1>(lr.d[a]);
+                        enter = box_decide(nd.bbox, lr, lrc, tmin, tmax);
+                    }
                     if (cp == 0) {  // skips that cannot change this lane's answer (see header)
                         if (may_skip_behind && behind(tmax)) enter = false;
                         if (!kShadow && best >= 0 && tmin > best_t + 1e-6 * (1.0 + fabs(best_t))) enter = false;
                     }
-                    if (!enter) resume = nd.skip;
                 }
+                if (active && !enter) resume = nd.skip;
                 if (__ballot(enter) == 0) {
                     i = nd.skip;
                     continue;
                 }
-                if (xf >= 0) {
+                if (nd.has_xf) {
                     if (sp >= S.xf_depth) {  // cannot happen: xf_depth is exact (upload)
                         err |= kErrXformDepth;
                         resume = kDone;
@@ -305,7 +413,11 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                     }
                     if ((threadIdx.x & 63) == 0) W.xn[sp] = i;
                     ++sp;
-                    cur = lr;
+                    xf_end = nd.skip;
+                    cur = xf_ray_walk(nd.m, cur);
+#if FRT_PREFILTER
+                    frame_cache(cur, fc);
+#endif
                 }
                 if constexpr (kCsg) {
                     if (type == FRT_CSG || cp > 0) {
@@ -319,14 +431,21 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                         W.cs[cp * kTraceBlock] = n;
                         W.ca[cp * kTraceBlock] = n;
                         ++cp;
+                        c_node = i;
+                        c_skip = nd.skip;
+                        c_right = nd.right;
+                        c_type = type;
+                        c_op = nd.op;
                     }
                 }
                 ++i;
                 continue;
             }
-            if (active) {
+            if (may) {
+                const Ray lr = nd.has_xf ? xf_ray_walk(nd.m, cur) : cur;
                 LeafHits H;
-                leaf_hits<kTorus>(nd, S.prim, lr, H);
+                if (kShadow && cp == 0 && type == FRT_CUBE && !(S.walk_flags & 4)) cube_hits_for_decisions(lr, distance, H);
+                else leaf_hits<kTorus>(type, S.prim + nd.prim, lr, H);
                 if (kCsg && cp > 0) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -362,7 +481,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                         }
                     }
                     if (stop_here) {
-                        result = blocked && S.casts[i] ? 1 : 0;
+                        result = blocked && nd.casts ? 1 : 0;
                         resume = kDone;
                     }
                 }
