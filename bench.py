@@ -39,9 +39,10 @@ DEFAULT_SCENE = "cornell_direct_800_4x4"
 CPU_SAMPLE_SCENE = "cornell_direct_200_4x4_t16"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
-# algorithmic bytes per k_shadow lane / per shaded node ("byte model")
-SHADOW_BYTES_PER_LANE = 24.0        # the light-cache point (3 doubles)
-SHADOW_BYTES_PER_NODE = 36.0 + 4.0  # over_point + key + material of the node, + the count word
+# algorithmic HBM bytes of k_shadow ("byte model"), reported by the engine per frame as
+# stats.shadow_kernel_bytes: per shaded path node the NodeRec head it reads (over_point, key,
+# material, padding: 48 B) and one 4-byte unshadowed count per light it writes. Light points and
+# sample tables (a few KB) stay in cache and are not counted.
 
 
 def log(*a):
@@ -164,9 +165,7 @@ def main():
         avg_ms = kernel_ms[dom] / max(1, launches[dom])
         roof = None
         if dom == "shadow":
-            lanes_per_frame = last["shadow_rays"]
-            nodes_per_frame = last["hits"]
-            bytes_per_frame = lanes_per_frame * SHADOW_BYTES_PER_LANE + nodes_per_frame * SHADOW_BYTES_PER_NODE
+            bytes_per_frame = last["shadow_kernel_bytes"]  # engine-side byte model (see above)
             per_launch = bytes_per_frame / max(1, launches[dom] / args.steps)
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

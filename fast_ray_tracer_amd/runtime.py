@@ -41,6 +41,7 @@ class FrameStats(ctypes.Structure):
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
             "hits": int(self.hits), "errors": int(self.errors), "render_ms": float(self.render_ms),
+            "shadow_kernel_bytes": float(self.shadow_kernel_bytes),
             "kernel_ms": {names[i]: float(self.kernel_ms[i]) for i in range(8) if self.kernel_launches[i]},
             "kernel_launches": {names[i]: int(self.kernel_launches[i]) for i in range(8) if self.kernel_launches[i]},
         }
