@@ -38,11 +38,12 @@ ASSETS = os.path.join(GOLDEN, "assets")
 DEFAULT_SCENE = "cornell_direct_800_4x4"
 CPU_SAMPLE_SCENE = "cornell_direct_200_4x4_t16"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PMC_TRAFFIC_FILE = "r01_pmc_traffic.json"  # FETCH_SIZE + MemWrites32B of k_shadow, per launch
 
 # algorithmic HBM bytes of k_shadow ("byte model"), reported by the engine per frame as
-# stats.shadow_kernel_bytes: per shaded path node the NodeRec head it reads (over_point, key,
-# material, padding: 48 B) and one 4-byte unshadowed count per light it writes. Light points and
-# sample tables (a few KB) stay in cache and are not counted.
+# stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point,
+# key, material; one cache line) and one 4-byte unshadowed count per light it writes. Light points
+# and sample tables (a few KB) stay in cache and are not counted.
 
 
 def log(*a):
@@ -170,7 +171,14 @@ def main():
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": "k_shadow",
-                    "avg_launch_ms": round(avg_ms, 4)}
+                    "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": round(per_launch)}
+            # HBM bytes per launch from the committed PMC passes of this kernel (tools/profile_round.sh)
+            pmc = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
+            if os.path.exists(pmc):
+                t = json.load(open(pmc))
+                if t.get("kernel") == "k_shadow" and t.get("workload") == args.scene:
+                    roof["traffic"] = round(t["traffic_bytes_per_launch"])
+                    roof["traffic_source"] = "profiles/" + PMC_TRAFFIC_FILE
         else:
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": dom, "avg_launch_ms": round(avg_ms, 4)}

@@ -39,9 +39,7 @@ namespace frt {
 
 constexpr int kBlock = 256;
 
-// path-node record of one level; node i of level d belongs to queued ray i.
-// The 48 bytes k_shadow reads (over_point, key, material) lead the record, so
-// the 100 shadow lanes of a node pull one cache line instead of two.
+// path-node record of one level; node i of level d belongs to queued ray i
 struct NodeRec {
     double over_point[3];
     uint64_t key;     // (global sample << 12) | heap code of the path node
@@ -56,6 +54,17 @@ struct NodeRec {
     double Ns, over_d, rf;
 };
 static_assert(sizeof(NodeRec) == 216, "NodeRec layout");
+
+// what k_shadow reads of a path node, one 64-byte line per node (the shadow
+// pass re-reads it from 100 lanes; keeping it apart from the 216-byte NodeRec
+// keeps the pass's HBM traffic at one line per node)
+struct alignas(64) ShadowHead {
+    double over_point[3];
+    uint64_t key;
+    int32_t material;  // -1: the ray missed
+    int32_t pad[5];
+};
+static_assert(sizeof(ShadowHead) == 64, "ShadowHead layout");
 
 struct QueuedRay {
     double o[3];
@@ -161,6 +170,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
 // prepare_computations + spawn of the reflection / refraction rays (renderer.c:369-605)
 __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
                                                     const HitRec* __restrict__ hits, NodeRec* __restrict__ rec,
+                                                    ShadowHead* __restrict__ heads,
                                                     QueuedRay* __restrict__ next_q, int64_t next_cap,
                                                     unsigned long long* next_count, unsigned long long* counters,
                                                     unsigned* err) {
@@ -186,6 +196,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
         rec[node].material = -1;
         rec[node].parent = parent;
         rec[node].slot = slot;
+        heads[node].material = -1;
         return;
     }
     Hit h{hr.t, -1, -1, hr.node};
@@ -281,6 +292,12 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
     }
     nr.flags = flags;
     rec[node] = nr;
+    ShadowHead hd;
+    for (int k = 0; k < 3; ++k) hd.over_point[k] = c.over_point[k];
+    hd.key = key;
+    hd.material = c.material;
+    for (int k = 0; k < 5; ++k) hd.pad[k] = 0;
+    heads[node] = hd;
 }
 
 // one lane per (node, light sample j); lanes of a node are consecutive
@@ -290,7 +307,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
 #define FRT_SHADOW_ATTR
 #endif
 template <int kFeat>
-__global__ void __launch_bounds__(kTraceBlock) FRT_SHADOW_ATTR k_shadow(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
+__global__ void __launch_bounds__(kTraceBlock) FRT_SHADOW_ATTR k_shadow(DevScene S, Batch B, const ShadowHead* __restrict__ shead, int64_t n,
                                                         const int32_t* __restrict__ j_light,
                                                         const int32_t* __restrict__ j_point, int32_t samples_per_node,
                                                         int32_t* __restrict__ counts, unsigned* err) {
@@ -306,7 +323,7 @@ __global__ void __launch_bounds__(kTraceBlock) FRT_SHADOW_ATTR k_shadow(DevScene
         const int j = (int)(tid % samples_per_node);
         light = j_light[j];
         const int pt = j_point[j];
-        const NodeRec* nr = rec + node;
+        const ShadowHead* nr = shead + node;
         if (nr->material >= 0) {
             live = true;
             const frt_light& L = S.lights[light];
@@ -519,6 +536,7 @@ struct frt_scene_handle {
     // work buffers (grow on demand)
     struct Level {
         frt::NodeRec* rec = nullptr;
+        frt::ShadowHead* head = nullptr;
         frt::QueuedRay* q = nullptr;
         double* surface = nullptr;
         double* child = nullptr;
@@ -816,6 +834,7 @@ void frt_scene_release(frt_scene_handle* h) {
     for (void* p : h->owned) hip_ignore(hipFree(p));
     for (auto& L : h->levels) {
         hip_ignore(hipFree(L.rec));
+        hip_ignore(hipFree(L.head));
         hip_ignore(hipFree(L.q));
         hip_ignore(hipFree(L.surface));
         hip_ignore(hipFree(L.child));
@@ -838,6 +857,8 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     if (need <= L.cap) return 0;
     int64_t nc = std::max<int64_t>(need, L.cap * 2);
     hip_ignore(hipFree(L.rec));
+    hip_ignore(hipFree(L.head));
+    L.head = nullptr;
     hip_ignore(hipFree(L.q));
     hip_ignore(hipFree(L.surface));
     hip_ignore(hipFree(L.child));
@@ -848,6 +869,7 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     L.child = nullptr;
     L.counts = nullptr;
     FRT_HIP(hipMalloc((void**)&L.rec, nc * sizeof(frt::NodeRec)));
+    FRT_HIP(hipMalloc((void**)&L.head, nc * sizeof(frt::ShadowHead)));
     FRT_HIP(hipMalloc((void**)&L.q, nc * sizeof(frt::QueuedRay)));
     FRT_HIP(hipMalloc((void**)&L.surface, nc * 12 * sizeof(double)));
     FRT_HIP(hipMalloc((void**)&L.child, nc * 24 * sizeof(double)));
@@ -919,13 +941,13 @@ static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::Qu
 }
 
 template <int F>
-static void launch_shadow_f(frt_scene_handle* h, const frt::Batch& B, const frt::NodeRec* rec, int64_t n, int32_t* counts) {
+static void launch_shadow_f(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts) {
     const int64_t work = n * h->samples_per_node;
     hipLaunchKernelGGL(frt::k_shadow<F>, dim3(grid_for(work, frt::kTraceBlock)), dim3(frt::kTraceBlock), h->lds_bytes,
                        h->stream, h->S, B, rec, n, h->j_light, h->j_point, h->samples_per_node, counts, h->err);
 }
 
-static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::NodeRec* rec, int64_t n, int32_t* counts) {
+static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts) {
     switch (h->S.features & 3) {
     case 0: launch_shadow_f<0>(h, B, rec, n, counts); break;
     case 1: launch_shadow_f<1>(h, B, rec, n, counts); break;
@@ -1010,12 +1032,12 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
             {
                 KTimer t(h, st, 6);
                 hipLaunchKernelGGL(k_prepare, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
-                                   L.rec, N.q, N.cap, h->counters + d + 1, h->counters + 16, h->err);
+                                   L.rec, L.head, N.q, N.cap, h->counters + d + 1, h->counters + 16, h->err);
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.include_direct && h->samples_per_node > 0) {
                 KTimer t(h, st, 1);
-                launch_shadow(h, B, L.rec, n, L.counts);
+                launch_shadow(h, B, L.head, n, L.counts);
                 FRT_HIP(hipGetLastError());
             }
             {
@@ -1068,9 +1090,9 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         st->pruned_secondary = host_counters[16];
         st->hits = host_counters[17];
         st->shadow_rays = h->S.cfg.include_direct ? host_counters[17] * (uint64_t)h->samples_per_node : 0;
-        // DESIGN.md byte model: per shaded node the 48-byte NodeRec head read + one 4-byte count per light written
+        // DESIGN.md byte model: per shaded node its 64-byte ShadowHead read + one 4-byte count per light written
         st->shadow_kernel_bytes =
-            h->S.cfg.include_direct && h->samples_per_node > 0 ? (double)host_counters[17] * (48.0 + 4.0 * h->S.num_lights) : 0.0;
+            h->S.cfg.include_direct && h->samples_per_node > 0 ? (double)host_counters[17] * (64.0 + 4.0 * h->S.num_lights) : 0.0;
         st->errors = err;
         collect_timings(h, st);
     }
