@@ -201,8 +201,10 @@ __device__ __forceinline__ bool box_may_hit(const double* bb, const Ray& r, cons
 // origin strictly inside the box: every slab gives t0 < 0 < t1 (signs of IEEE
 // quotients are exact; the EPSILON branch gives -inf / +inf), so the reference's
 // box test reports a hit with tmin < 0 < tmax — decided without any slab arithmetic
+// (all six comparisons evaluated: no short-circuit chain of dependent loads)
 __device__ __forceinline__ bool origin_inside(const double* bb, const Ray& r) {
-    return bb[0] < r.o[0] && r.o[0] < bb[3] && bb[1] < r.o[1] && r.o[1] < bb[4] && bb[2] < r.o[2] && r.o[2] < bb[5];
+    return (bb[0] < r.o[0]) & (r.o[0] < bb[3]) & (bb[1] < r.o[1]) & (r.o[1] < bb[4]) & (bb[2] < r.o[2]) &
+           (r.o[2] < bb[5]);
 }
 
 // Could a local direction component (row a of the node's inverse transform
