@@ -136,6 +136,7 @@ struct HitRec {
     double t;
     int32_t node;  // -1: miss
     int32_t pad;
+    double n1, n2;  // refractive indices either side of the hit (containers)
 };
 
 extern __shared__ __align__(16) char frt_walk_smem[];
@@ -162,8 +163,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
     }
     unsigned e = 0;
     double t;
-    const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e);
-    if (live) hits[i] = HitRec{t, node, 0};
+    double n12[2];
+    const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12);
+    if (live) hits[i] = HitRec{t, node, 0, n12[0], n12[1]};
     if (e) atomicOr(err, e);
 }
 
@@ -202,6 +204,8 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
     Hit h{hr.t, -1, -1, hr.node};
     Comps c;
     prepare(S, r, h, c);
+    c.n1 = hr.n1;
+    c.n2 = hr.n2;
     atomicAdd(counters + 1, 1ull);  // shaded path nodes
     const frt_material& M = S.materials[c.material];
     NodeRec nr;
@@ -625,7 +629,6 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     if (sc->camera.aperture_type != 6 /* POINT_APERTURE */ && sc->camera.aperture_size != 0.0)
         return fail("frt_scene_upload: thin-lens apertures are not supported yet");
     if (sc->camera.jitter) return fail("frt_scene_upload: jittered camera sampling is not supported yet");
-    if (!sc->config.all_ni_one) return fail("frt_scene_upload: refractive indices != 1 are not supported yet");
     FRT_HIP(hipSetDevice(device));
     frt_scene_handle* h = new frt_scene_handle();
     h->device = device;

@@ -223,9 +223,48 @@ constexpr int kDone = 0x7fffffff;  // resume index of a lane whose walk has fini
 //   kShadow = false: returns the closest-hit leaf (-1 = miss), its t in best_t.
 //   kShadow = true:  returns 1 if shadowed (is_shadowed), else 0.
 // Lanes that should not trace pass live = false (they still take part).
+// Refractive containers (prepare_computations, renderer.c:404-447) for the
+// closest hit: the reference walks the full sorted list up to the hit,
+// toggling objects in and out of an ordered container. Every entry before the
+// hit has t <= 0 (the hit is the first positive one), and all entries of an
+// object are emitted together, so the container at the hit is determined by,
+// per object, the parity of its t <= 0 entries and the sort key (t, node,
+// index) of its last one: the container's last element is the present object
+// with the greatest key. The walk keeps the two greatest present objects.
+struct ContainerTop2 {
+    double t1, t2;
+    int n1, i1, n2, i2;  // node -1: none
+    __device__ __forceinline__ void init() {
+        n1 = n2 = -1;
+        t1 = t2 = 0.0;
+        i1 = i2 = 0;
+    }
+    __device__ __forceinline__ static bool greater(double ta, int na, int ia, double tb, int nb, int ib) {
+        return ta > tb || (ta == tb && (na > nb || (na == nb && ia > ib)));
+    }
+    __device__ __forceinline__ void offer(double t, int node, int idx) {
+        if (n1 < 0 || greater(t, node, idx, t1, n1, i1)) {
+            t2 = t1;
+            n2 = n1;
+            i2 = i1;
+            t1 = t;
+            n1 = node;
+            i1 = idx;
+        } else if (n2 < 0 || greater(t, node, idx, t2, n2, i2)) {
+            t2 = t;
+            n2 = node;
+            i2 = idx;
+        }
+    }
+};
+
+__device__ __forceinline__ double node_ni(const DevScene& S, int node) {
+    return node >= 0 ? S.materials[S.nodes[node].material].Ni : 1.0;
+}
+
 template <bool kShadow, int kFeat>
 __device__ int walk(const DevScene& S, const Ray& world, double distance, bool live, double& best_t, char* smem,
-                    unsigned& err) {
+                    unsigned& err, double* n12 = nullptr) {
     constexpr bool kCsg = (kFeat & kFeatCsg) != 0;
     constexpr bool kTorus = (kFeat & kFeatTorus) != 0;
     constexpr int kNone = 0x7fffffff;
@@ -233,6 +272,10 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
     int best = -1;
     int result = 0;
     best_t = 0.0;
+    const bool cont = !kShadow && !S.cfg.all_ni_one;  // refractive containers needed
+    ContainerTop2 ct;
+    ct.init();
+    bool best_present = false;
 #ifdef FRT_WALK_STATS
     {
         const unsigned long long lv = __ballot(live);
@@ -246,7 +289,9 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
         if (__ballot(live) == 0) break;
         const int root = S.roots[ri];
         const int end = S.wn[root].skip;
-        const bool may_skip_behind = !kShadow || ri == S.num_roots - 1;
+        // entries behind the origin matter for the containers (closest hit) and, for shadow
+        // rays, for the "first world shape with entries" rule before the last world shape
+        const bool may_skip_behind = kShadow ? ri == S.num_roots - 1 : !cont;
         // uniform walk state; the tops of both frame stacks are cached here
         int sp = 0, xf_end = kNone;                             // transform frames
         int cp = 0, c_node = 0, c_skip = kNone, c_right = 0;   // composite frames (inside a CSG unit)
@@ -289,11 +334,33 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                     // a CSG unit of the main walk is complete: the lane's list is [0, n)
                     if (resume != kDone) {
                         if (!kShadow) {
+                            int unit_best = -1;
                             for (int k = 0; k < n; ++k) {
                                 const double t = W.T(k);
                                 if (t > 0 && (best < 0 || t < best_t)) {
                                     best_t = t;
                                     best = W.N(k);
+                                    unit_best = best;
+                                }
+                            }
+                            if (cont) {
+                                // per node of the unit: parity of its t <= 0 entries and its last one
+                                for (int k = 0; k < n; ++k) {
+                                    const int nk = W.N(k);
+                                    int cnt = 0, last = -1;
+                                    for (int q = 0; q < n; ++q) {
+                                        if (W.N(q) == nk && W.T(q) <= 0) {
+                                            ++cnt;
+                                            if (last < 0 || W.T(q) > W.T(last) || (W.T(q) == W.T(last) && q > last))
+                                                last = q;
+                                        }
+                                    }
+                                    if (last == k && (cnt & 1)) ct.offer(W.T(k), nk, k);
+                                }
+                                if (unit_best >= 0) {
+                                    int cnt = 0;
+                                    for (int q = 0; q < n; ++q) cnt += (W.N(q) == unit_best && W.T(q) <= 0) ? 1 : 0;
+                                    best_present = (cnt & 1) != 0;
                                 }
                             }
                         } else if (n > 0) {
@@ -460,13 +527,32 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                         }
                     }
                 } else if (!kShadow) {
+                    bool took = false;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const double t = H.t.at(j);
                         if (j < H.t.n && t > 0 && (best < 0 || t < best_t)) {
                             best_t = t;
                             best = i;
+                            took = true;
                         }
+                    }
+                    if (cont) {
+                        int cnt = 0, last = -1;
+                        double tl = 0.0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const double t = H.t.at(j);
+                            if (j < H.t.n && t <= 0) {
+                                ++cnt;
+                                if (last < 0 || t >= tl) {
+                                    tl = t;
+                                    last = j;
+                                }
+                            }
+                        }
+                        if (cnt & 1) ct.offer(tl, i, last);
+                        if (took) best_present = (cnt & 1) != 0;
                     }
                 } else if (H.t.n > 0) {
                     any_entry = true;
@@ -490,6 +576,14 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
         }
         if (kShadow && live && resume != kDone && any_entry) live = false;  // first world shape with entries ends it
         if (resume == kDone) live = false;
+    }
+    if (!kShadow && n12 != nullptr) {
+        n12[0] = 1.0;
+        n12[1] = 1.0;
+        if (cont && best >= 0) {
+            n12[0] = node_ni(S, ct.n1);
+            n12[1] = best_present ? (best == ct.n1 ? node_ni(S, ct.n2) : n12[0]) : node_ni(S, best);
+        }
     }
     return kShadow ? result : best;
 }

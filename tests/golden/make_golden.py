@@ -60,6 +60,8 @@ SCENES = {
     "area_light_test_100": ("scenes/area_light_test/area_light_test.yml", {"size": (100, 100), "cache": 1}),
     "reflect_refract_160x80": ("scenes/reflect_refract/reflect_refract.yml", {"size": (160, 80)}),
     "bump_map_100": ("scenes/bump_map_test/bump_map_test.yml", {"size": (100, 100)}),
+    # nested refraction: a glass sphere (Ni 1.5) holding an air bubble (Ni 1.0000034) -> refractive containers
+    "reflect_refract_test_150": ("scenes/reflect_refract_test/test.yml", {"size": (150, 150)}),
     # benchmark scene (BASELINE.json configs[2]: cornell_box 800x800, 4x4 CMJ, full recursion;
     # GI off, single-row area-light cache = the deterministic parity variant). No canvas golden:
     # the reference takes minutes here; parity is checked at the small sizes above.
