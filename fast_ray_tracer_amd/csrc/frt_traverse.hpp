@@ -105,6 +105,7 @@ enum ErrBits : unsigned {
     kErrXformDepth = 4u,
     kErrQueueOverflow = 8u,
     kErrContainer = 16u,
+    kErrAperture = 32u,
 };
 
 __device__ __forceinline__ const double* xform_of(const DevScene& S, int x) { return S.xforms + 16 * (size_t)x; }

@@ -136,6 +136,7 @@ static struct {
     size_t usteps, vsteps;
     bool jitter;
     int captured;
+    unsigned short drand48_state[3];
 } g_capture;
 
 Canvas
@@ -153,6 +154,14 @@ frt_capture_render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool
     g_capture.vsteps = vsteps;
     g_capture.jitter = jitter;
     g_capture.captured = 1;
+    {
+        /* snapshot drand48's state at the render_multi call (the reference's
+         * jitter / aperture draws start from here); seed48 returns the old state */
+        unsigned short probe[3] = {0, 0, 0};
+        unsigned short *old = seed48(probe);
+        memcpy(g_capture.drand48_state, old, sizeof(g_capture.drand48_state));
+        seed48(g_capture.drand48_state);
+    }
     Canvas c = canvas_alloc(1, 1, false, NULL);
     memset(c->arr, 0, sizeof(Color));
     return c;
@@ -181,6 +190,8 @@ World frt_captured_world(void) { return g_capture.w; }
 size_t frt_captured_usteps(void) { return g_capture.usteps; }
 size_t frt_captured_vsteps(void) { return g_capture.vsteps; }
 int frt_captured_jitter(void) { return g_capture.jitter ? 1 : 0; }
+void frt_captured_drand48(unsigned short out[3]) { memcpy(out, g_capture.drand48_state, sizeof(g_capture.drand48_state)); }
+void frt_set_drand48(const unsigned short in[3]) { seed48((unsigned short *)in); }
 size_t frt_camera_hsize(Camera c) { return c->hsize; }
 size_t frt_camera_vsize(Camera c) { return c->vsize; }
 

@@ -108,6 +108,9 @@ class Scene:
         self.usteps = int(lib.frt_captured_usteps())
         self.vsteps = int(lib.frt_captured_vsteps())
         self.jitter = bool(lib.frt_captured_jitter())
+        st = (ctypes.c_ushort * 3)()
+        lib.frt_captured_drand48(st)
+        self.drand48_state = tuple(st)  # glibc drand48 state at the render_multi call (stochastic checks)
         self.width = int(lib.frt_camera_hsize(self.camera))
         self.height = int(lib.frt_camera_vsize(self.camera))
         self.name = os.path.splitext(os.path.basename(scene_so))[0]

@@ -52,6 +52,9 @@ def render(scene, row_begin: int = 0, row_end: int | None = None, threads: int =
     out = np.zeros((row_end - row_begin, scene.width, 4), dtype=np.float64)
     st = OracleStats()
     threads = threads or min(8, os.cpu_count() or 1)
+    # drand48 (pixel jitter, aperture samples) continues from the state the scene's main() left,
+    # as in the reference's executable; with one thread the draw order is the reference's
+    host_lib().frt_set_drand48((ctypes.c_ushort * 3)(*scene.drand48_state))
     rc = lib.frt_oracle_render_rows(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter,
                                     row_begin, row_end, threads, out.ctypes.data_as(ctypes.c_void_p),
                                     ctypes.byref(st))

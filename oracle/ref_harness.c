@@ -14,6 +14,16 @@
 Canvas
 frt_ref_render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
 {
+    /* statistical goldens: a second, independent reference run re-seeds drand48
+     * (pixel jitter, aperture samples) after the scene is built */
+    const char *seed_env = getenv("FRT_REF_DRAND_SEED");
+    if (seed_env != NULL) {
+        unsigned long long sd = strtoull(seed_env, NULL, 10);
+        unsigned short s48[3] = {(unsigned short)(sd & 0xffff), (unsigned short)((sd >> 16) & 0xffff),
+                                 (unsigned short)((sd >> 32) & 0xffff)};
+        seed48(s48);
+        srand((unsigned)(sd & 0x7fffffff));  /* area-light cache rows: rand() % cache_size */
+    }
     struct timespec a, b;
     clock_gettime(CLOCK_MONOTONIC, &a);
     Canvas c = render_multi(cam, w, usteps, vsteps, jitter);

@@ -49,6 +49,13 @@ def load_scene(name):
     return _scenes[name]
 
 
+def fresh_scene(name):
+    """Capture a golden scene anew (not cached): the libc RNG state right after its main()."""
+    from fast_ray_tracer_amd import build
+    from fast_ray_tracer_amd.runtime import Scene
+    return Scene(build.build_scene(os.path.join(GOLDEN, "scenes", name + ".c")), asset_root=ASSETS)
+
+
 def load_golden_canvas(name):
     import numpy as np
     e = golden_index()[name]

@@ -40,6 +40,8 @@ REF = os.environ.get("FRT_REFERENCE_DIR", "/root/reference")
 SCRATCH = "/tmp/frt_golden"
 REF_COPY = os.path.join(SCRATCH, "ref")
 
+STOCHASTIC_SEEDS = [12345, 777, 31337, 4242, 2718]
+
 # name -> (yaml, overrides, golden canvas kind)
 #   size: (w, h); steps: (u, v); cache: area-light cache-size; threads: reference pool size
 SCENES = {
@@ -62,6 +64,22 @@ SCENES = {
     "bump_map_100": ("scenes/bump_map_test/bump_map_test.yml", {"size": (100, 100)}),
     # nested refraction: a glass sphere (Ni 1.5) holding an air bubble (Ni 1.0000034) -> refractive containers
     "reflect_refract_test_150": ("scenes/reflect_refract_test/test.yml", {"size": (150, 150)}),
+    # stochastic camera paths (drand48 in the reference; statistical parity): independent
+    # reference runs (default libc RNG state + re-seeded ones) are stored as refs[k]
+    "checkered_sphere_jitter_100": ("scenes/checkered_sphere/checkered_sphere.yml",
+                                    {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
+                                     "extra_seeds": STOCHASTIC_SEEDS}),
+    # the benchmark scene as shipped (cache-size 65535, light rows drawn with rand()), camera jitter
+    # on, small image: statistical parity of the stochastic direct-lighting path (BASELINE cfg3-ii)
+    "cornell_shipped_48_4x4": ("scenes/cornell_box/cornell_box.yml",
+                               {"size": (48, 48), "steps": (4, 4), "jitter": True, "gi_off": True, "threads": 1,
+                                "extra_seeds": STOCHASTIC_SEEDS}),
+    # global illumination (photon map + final gather) as shipped: main.c only, the input of the
+    # "unsupported features fail loudly" test (no device path yet)
+    "cornell_gi_16": ("scenes/cornell_box/cornell_box.yml", {"size": (16, 16), "no_golden": True}),
+    "checkered_sphere_dof_100": ("scenes/checkered_sphere/checkered_sphere.yml",
+                                 {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
+                                  "aperture": (["CIRCULAR_APERTURE", 1.0], 0.4), "extra_seeds": STOCHASTIC_SEEDS}),
     # benchmark scene (BASELINE.json configs[2]: cornell_box 800x800, 4x4 CMJ, full recursion;
     # GI off, single-row area-light cache = the deterministic parity variant). No canvas golden:
     # the reference takes minutes here; parity is checked at the small sizes above.
@@ -88,6 +106,11 @@ def apply_overrides(tree, name, ov):
             cam["usteps"], cam["vsteps"] = ov["steps"]
             ap = cam.setdefault("aperture", {})
             ap["usteps"], ap["vsteps"] = ov["steps"]
+        if "jitter" in ov:
+            cam.setdefault("aperture", {})["jitter"] = ov["jitter"]
+        if "aperture" in ov:  # (type list, size)
+            ap = cam.setdefault("aperture", {})
+            ap["type"], ap["size"] = ov["aperture"]
     if "cache" in ov:
         for light in find(tree, lambda it: it.get("add") == "light" and ("corner" in it or "radius" in it)):
             light["cache-size"] = ov["cache"]
@@ -188,8 +211,22 @@ def main(names):
             "ppm_sha256": sha256(out_base + ".ppm"), "png_sha256": sha256(out_base + ".png"),
             "canvas_sum": [float(x) for x in canvas.reshape(-1, 3).sum(axis=0)],
         })
+        arrays = {"canvas": canvas}
+        if ov.get("extra_seeds"):
+            # further independent reference renders (drand48 / rand() re-seeded by the harness)
+            extra = []
+            for sd in ov["extra_seeds"]:
+                env2 = dict(env, FRT_REF_DRAND_SEED=str(sd))
+                r2 = subprocess.run([binary], cwd=REF_COPY, env=env2, stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.PIPE, text=True)
+                if r2.returncode != 0:
+                    raise RuntimeError("extra reference run failed for %s: %s" % (name, r2.stderr[-2000:]))
+                extra.append(np.fromfile(canvas_bin, dtype=np.float64).reshape(h, w, 4)[:, :, :3])
+            arrays["refs"] = np.stack([canvas] + extra)
+            entry["stochastic"] = True
+            entry["extra_seeds"] = list(ov["extra_seeds"])
         if not ov.get("hash_only"):
-            np.savez_compressed(os.path.join(HERE, name + ".npz"), canvas=canvas)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
             entry["canvas"] = name + ".npz"
         index[name] = entry
         print("%-28s %4dx%-4d %.2fs (wall %.1fs)" % (name, w, h, stats["render_multi_seconds"], time.time() - t0))
