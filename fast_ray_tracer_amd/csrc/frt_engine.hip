@@ -238,10 +238,11 @@ extern __shared__ __align__(16) char frt_walk_smem[];
 // closest hit of every ray of one level (level 0: camera rays generated in place)
 template <int kFeat>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
-                                                       HitRec* __restrict__ hits, unsigned* err) {
-    // every lane of the wave takes part in the (wave-coherent) walk
+                                                       HitRec* __restrict__ hits, unsigned* err, int filter_casts) {
+    // every lane of the wave takes part in the (wave-coherent) walk; queued rays with
+    // parent < -1 are placeholders (final-gather slots of nodes without a gather)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = i < n;
+    const bool live = i < n && (q == nullptr || q[i].parent >= -1);
     Ray r{{0, 0, 0}, {0, 0, 1}};
     unsigned e = 0;
     if (live) {
@@ -258,8 +259,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
     }
     double t;
     double n12[2];
-    const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12);
-    if (live) hits[i] = HitRec{t, node, 0, n12[0], n12[1]};
+    const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12, filter_casts != 0);
+    if (i < n) hits[i] = live ? HitRec{t, node, 0, n12[0], n12[1]} : HitRec{0.0, -1, 0, 1.0, 1.0};
     if (e) atomicOr(err, e);
 }
 
@@ -616,6 +617,355 @@ __global__ void __launch_bounds__(kBlock) k_resolve(const double* __restrict__ s
     o[3] = 0.0;
 }
 
+
+}  // namespace frt
+
+#include "frt_gi.hpp"
+
+namespace frt {
+
+// =====================================================================
+// global illumination: photon tracing (photon_tracer.c) and the GI terms
+// of shade_hit (renderer.c:727-770)
+// =====================================================================
+
+constexpr uint64_t kTagPhoton = 0x9a0be7f1d3c2b5a1ULL;
+constexpr uint64_t kTagGather = 0x51f15e0ddeadc0deULL;
+
+struct StoredPhoton {
+    double pos[3], power[3], dir[3];
+    uint64_t key;  // emission index << 8 | bounce (the reference's storage order)
+};
+
+__device__ __forceinline__ bool any_positive(const double* c) { return c[0] > 0 || c[1] > 0 || c[2] > 0; }
+
+// emit_photon (light.c:14-99): one photon of light L, emission index e
+__device__ inline void emit_photon(const DevScene& S, const frt_light& L, uint64_t seed, uint64_t e, Ray& r) {
+    if (L.type == FRT_POINT_LIGHT) {
+        double d[3];
+        for (int a = 0; a < 4096; ++a) {  // rejection in the unit ball (light.c:80-92)
+            for (int k = 0; k < 3; ++k) d[k] = 2 * rng_uniform(seed, e, 8 + 3 * a + k) - 1;
+            if (!(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] > 1)) break;
+        }
+        for (int k = 0; k < 3; ++k) {
+            r.o[k] = L.position[k];
+            r.d[k] = d[k];
+        }
+        return;
+    }
+    if (L.type == FRT_HEMISPHERE_LIGHT) {
+        for (int k = 0; k < 3; ++k) r.o[k] = L.position[k];
+    } else {  // area / circle: a random point of a random cache row (light_surface_points + rand())
+        const uint64_t h1 = mix64(seed ^ mix64(e * 0x9e3779b97f4a7c15ULL + 1));
+        const uint64_t h2 = mix64(seed ^ mix64(e * 0x9e3779b97f4a7c15ULL + 2));
+        const int64_t row = (int64_t)(h1 % (uint64_t)(L.rows > 0 ? L.rows : 1));
+        const int64_t pt = (int64_t)(h2 % (uint64_t)(L.num_samples > 0 ? L.num_samples : 1));
+        const double* p = S.light_points + L.points + 3 * (row * L.num_samples + pt);
+        for (int k = 0; k < 3; ++k) r.o[k] = p[k];
+    }
+    double nt[3], nb[3];
+    coordinate_system(L.normal, nt, nb);
+    hemisphere_dir(L.normal, nt, nb, rng_uniform(seed, e, 3), rng_uniform(seed, e, 4), r.d);
+}
+
+// photons of light `light` with emission indices e0 .. e0+n-1 -> the first photon queue
+__global__ void __launch_bounds__(kBlock) k_photon_emit(DevScene S, uint64_t seed, int light, uint64_t e0, int64_t n,
+                                                        QueuedRay* __restrict__ q, double* __restrict__ power) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const frt_light& L = S.lights[light];
+    const uint64_t e = e0 + (uint64_t)i;
+    Ray r;
+    emit_photon(S, L, seed, e, r);
+    QueuedRay qr;
+    for (int k = 0; k < 3; ++k) {
+        qr.o[k] = r.o[k];
+        qr.d[k] = r.d[k];
+        power[3 * i + k] = L.intensity[k];
+    }
+    qr.key = e;
+    qr.parent = -1;
+    qr.slot = 0;  // bit0 had_diffuse, bit1 had_specular
+    q[i] = qr;
+}
+
+// power_at's hit half + photon_hit (photon_tracer.c:114-182) for one bounce
+__global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed, int map, int depth,
+                                                       const QueuedRay* __restrict__ q, const double* __restrict__ power,
+                                                       int64_t n, const HitRec* __restrict__ hits,
+                                                       QueuedRay* __restrict__ next_q, double* __restrict__ next_power,
+                                                       unsigned long long* next_count, int64_t next_cap,
+                                                       StoredPhoton* __restrict__ store, unsigned long long* store_count,
+                                                       int64_t store_cap, unsigned* err) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const HitRec hr = hits[i];
+    if (hr.node < 0) return;
+    const QueuedRay qr = q[i];
+    Ray r;
+    for (int k = 0; k < 3; ++k) {
+        r.o[k] = qr.o[k];
+        r.d[k] = qr.d[k];
+    }
+    double pp[3] = {power[3 * i], power[3 * i + 1], power[3 * i + 2]};
+    if (pp[0] <= 0 && pp[1] <= 0 && pp[2] <= 0) return;  // shadow / dead photons
+    Hit h{hr.t, -1, -1, hr.node};
+    Comps c;
+    prepare(S, r, h, c);
+    c.n1 = hr.n1;
+    c.n2 = hr.n2;
+    const frt_material& M = S.materials[c.material];
+    const bool had_diffuse = (qr.slot & 1) != 0, had_specular = (qr.slot & 2) != 0;
+    const uint64_t e = qr.key;
+    const double avg_d = (c.Kd[0] + c.Kd[1] + c.Kd[2]) / 3.0;
+    if (any_positive(c.Kd)) {
+        const bool store_it = map == 0 ? had_specular : had_diffuse;
+        if (store_it) {
+            const unsigned long long at = atomicAdd(store_count, 1ull);
+            if ((int64_t)at < store_cap) {
+                StoredPhoton sp;
+                for (int k = 0; k < 3; ++k) {
+                    sp.pos[k] = c.p[k];
+                    sp.power[k] = c.Kd[k] * pp[k];
+                    sp.dir[k] = r.d[k];  // the photon ray's direction (pm_store's dir)
+                }
+                sp.key = (e << 8) | (uint64_t)depth;
+                store[at] = sp;
+            } else {
+                atomicOr(err, kErrQueueOverflow);
+            }
+            if (map == 0) return;  // a caustic photon ends at its first diffuse store
+        }
+    }
+    // russian roulette (photon_tracer.c:154-179)
+    const double rr = rng_uniform(seed ^ 0x7u, e, 64 + (uint64_t)depth);
+    const double avg_s = (c.refl[0] + c.refl[1] + c.refl[2]) / 3.0;
+    const double avg_t = (M.Tf[0] + M.Tf[1] + M.Tf[2]) / 3.0;
+    int choice = -1;  // 0 diffuse, 1 specular, 2 refract
+    if (map == 1) {
+        const double total = avg_d + avg_s + avg_t;
+        if (rr * total < avg_d) choice = 0;
+        else if (rr * total < avg_d + avg_s) choice = 1;
+        else if (rr * total < avg_d + avg_s + avg_t) choice = 2;
+    } else {
+        const double total = avg_s + avg_t;
+        if (rr * total < avg_s) choice = 1;
+        else if (rr * total < avg_s + avg_t) choice = 2;
+    }
+    if (choice < 0) return;
+    QueuedRay nq;
+    double np[3];
+    int flags = qr.slot;
+    if (choice == 0) {  // reflect_photon_diffuse (photon_tracer.c:31-62)
+        for (int k = 0; k < 3; ++k) np[k] = c.Kd[k] * pp[k];
+        double nt[3], nb[3], d[3];
+        coordinate_system(c.normalv, nt, nb);
+        hemisphere_dir(c.normalv, nt, nb, rng_uniform(seed ^ 0x9u, e, 2 * (uint64_t)depth),
+                       rng_uniform(seed ^ 0x9u, e, 2 * (uint64_t)depth + 1), d);
+        for (int k = 0; k < 3; ++k) {
+            nq.o[k] = c.over_point[k];
+            nq.d[k] = d[k];
+        }
+        flags |= 1;
+    } else if (choice == 1) {  // reflect_photon_specular (photon_tracer.c:64-77)
+        if (!M.reflective) return;
+        const double sc = 1.0 / avg_s;
+        for (int k = 0; k < 3; ++k) {
+            np[k] = pp[k] * sc;
+            nq.o[k] = c.over_point[k];
+            nq.d[k] = c.reflectv[k];
+        }
+        flags |= 2;
+    } else {  // refract_photon (photon_tracer.c:81-112)
+        if (feq(M.Tr, 0.0)) return;
+        const double n_ratio = c.n1 / c.n2;
+        const double cos_i = dot3(c.eyev, c.normalv);
+        const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
+        if (sin2_t > 1.0) return;
+        const double cos_t = sqrt(1.0 - sin2_t);
+        const double s1 = n_ratio * cos_i - cos_t;
+        const double sc = 1.0 / avg_t;
+        for (int k = 0; k < 3; ++k) {
+            const double t1 = c.normalv[k] * s1;
+            const double t2 = c.eyev[k] * n_ratio;
+            nq.o[k] = c.under_point[k];
+            nq.d[k] = t1 - t2;
+            np[k] = pp[k] * sc;
+        }
+        flags |= 2;
+    }
+    const unsigned long long at = atomicAdd(next_count, 1ull);
+    if ((int64_t)at >= next_cap) {
+        atomicOr(err, kErrQueueOverflow);
+        return;
+    }
+    nq.key = e;
+    nq.parent = -1;
+    nq.slot = flags;
+    next_q[at] = nq;
+    for (int k = 0; k < 3; ++k) next_power[3 * at + k] = np[k];
+}
+
+// lighting_gi (renderer.c:863-892) / lighting_caustics (renderer.c:829-861) estimate at a surface point
+__device__ inline void photon_estimate(const PhotonMapDev& M, const DevScene& S, const double* point,
+                                       const double* eyev, double scale_num, double* est) {
+    const int64_t used = irradiance_estimate(M, point, eyev /* the reference passes eyev as the normal */,
+                                             S.cfg.irradiance_radius, S.cfg.irradiance_num, S.cfg.cone_filter_k, est);
+    if (used > 0) {
+        const double f = scale_num / (double)used;
+        for (int k = 0; k < 3; ++k) est[k] *= f;
+    }
+}
+
+// per shaded node: the visualisation term (lighting_gi) and the caustics term (renderer.c:740-761)
+__global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, const NodeRec* __restrict__ rec, int64_t n,
+                                                    double* __restrict__ gi_extra) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double* out = gi_extra + 6 * i;
+    for (int k = 0; k < 6; ++k) out[k] = 0.0;
+    const NodeRec& nr = rec[i];
+    if (nr.material < 0 || !any_positive(nr.Kd)) return;
+    const double edn = dot3(nr.eyev, nr.normalv);
+    if (S.cfg.visualize_photon_map) {  // lighting_gi, visualize branch: the raw estimate
+        double est[3];
+        photon_estimate(S.pmaps[1], S, nr.over_point, nr.eyev, 10.0 * (double)S.cfg.irradiance_num, est);
+        for (int k = 0; k < 3; ++k) out[k] = est[k];
+    }
+    if (S.cfg.include_caustics) {
+        double est[3];
+        photon_estimate(S.pmaps[0], S, nr.over_point, nr.eyev, 100.0, est);
+        if (S.cfg.visualize_photon_map) {
+            for (int k = 0; k < 3; ++k) out[3 + k] = est[k];
+        } else {
+            for (int k = 0; k < 3; ++k) {
+                double ck = nr.Kd[k] * est[k];
+                out[3 + k] = 0.0 + ck * edn;
+            }
+        }
+    }
+}
+
+// final_gather's rays (renderer.c:648-687): gu x gv cosine-weighted hemisphere
+// directions (a jittered CMJ pattern per gather) from over_point
+__global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed, const NodeRec* __restrict__ rec,
+                                                       int64_t node0, int64_t nodes, QueuedRay* __restrict__ gq) {
+    const int G = S.cfg.gi_usteps * S.cfg.gi_vsteps;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nodes * G) return;
+    const int64_t node = node0 + t / G;
+    const int slot = (int)(t % G);
+    const NodeRec& nr = rec[node];
+    QueuedRay qr;
+    qr.key = nr.key;
+    qr.slot = slot;
+    if (nr.material < 0 || !any_positive(nr.Kd)) {
+        qr.parent = -2;  // placeholder
+        for (int k = 0; k < 3; ++k) qr.o[k] = qr.d[k] = 0.0;
+        gq[t] = qr;
+        return;
+    }
+    double jit[2], nt[3], nb[3], d[3];
+    cmj_point(seed ^ kTagGather, nr.key, S.cfg.gi_usteps, S.cfg.gi_vsteps, slot % S.cfg.gi_usteps,
+              slot / S.cfg.gi_usteps, jit);
+    coordinate_system(nr.normalv, nt, nb);
+    hemisphere_dir(nr.normalv, nt, nb, jit[0], jit[1], d);
+    for (int k = 0; k < 3; ++k) {
+        qr.o[k] = nr.over_point[k];
+        qr.d[k] = d[k];
+    }
+    qr.parent = (int32_t)node;
+    gq[t] = qr;
+}
+
+// color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray, scaled by the sample's
+// first coordinate (final_gather: "scale by theta")
+__global__ void __launch_bounds__(kBlock) k_gather_shade(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
+                                                         const HitRec* __restrict__ hits, int64_t n,
+                                                         double* __restrict__ gather_col) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    double* out = gather_col + 3 * t;
+    out[0] = out[1] = out[2] = 0.0;
+    const QueuedRay qr = gq[t];
+    const HitRec hr = hits[t];
+    if (qr.parent < 0 || hr.node < 0) return;
+    Ray r;
+    for (int k = 0; k < 3; ++k) {
+        r.o[k] = qr.o[k];
+        r.d[k] = qr.d[k];
+    }
+    const int leaf = hr.node;
+    const frt_material& M = S.materials[S.nodes[leaf].material];
+    double p[3], diffuse[3];
+    for (int k = 0; k < 3; ++k) p[k] = r.o[k] + r.d[k] * hr.t;
+    if (M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, leaf, p, diffuse);
+    else copy3(M.Kd, diffuse);
+    double c[3] = {0, 0, 0};
+    if (any_positive(diffuse)) {
+        Hit h{hr.t, -1, -1, leaf};
+        Comps cp;
+        prepare(S, r, h, cp);
+        if (any_positive(cp.Kd)) {  // lighting_gi (renderer.c:863-892)
+            double est[3];
+            photon_estimate(S.pmaps[1], S, cp.over_point, cp.eyev, 10.0 * (double)S.cfg.irradiance_num, est);
+            if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
+                for (int k = 0; k < 3; ++k) c[k] = est[k] * kPi;  // shade_hit_gi: x pi
+            } else {
+                const double edn = dot3(cp.eyev, cp.normalv);
+                for (int k = 0; k < 3; ++k) {
+                    double dk = cp.Kd[k] * est[k];
+                    dk = dk * edn;
+                    c[k] = dk * kPi;  // shade_hit_gi: x pi
+                }
+            }
+        }
+    }
+    double jit[2];
+    cmj_point(seed ^ kTagGather, qr.key, S.cfg.gi_usteps, S.cfg.gi_vsteps, qr.slot % S.cfg.gi_usteps,
+              qr.slot / S.cfg.gi_usteps, jit);
+    for (int k = 0; k < 3; ++k) out[k] = c[k] * jit[0];
+}
+
+// final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd
+__global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, const NodeRec* __restrict__ rec, int64_t node0,
+                                                          int64_t nodes, const double* __restrict__ gather_col,
+                                                          double* __restrict__ fgather) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nodes) return;
+    const int64_t node = node0 + t;
+    const int G = S.cfg.gi_usteps * S.cfg.gi_vsteps;
+    const NodeRec& nr = rec[node];
+    double* out = fgather + 3 * node;
+    out[0] = out[1] = out[2] = 0.0;
+    if (nr.material < 0 || !any_positive(nr.Kd)) return;
+    double total[3] = {0, 0, 0};
+    for (int sl = 0; sl < G; ++sl)
+        for (int k = 0; k < 3; ++k) total[k] += gather_col[3 * (t * G + sl) + k];
+    const double sc = 2 * kPi / (double)G;
+    for (int k = 0; k < 3; ++k) out[k] = (total[k] * sc) * nr.Kd[k];
+}
+
+// shade_hit's GI block (renderer.c:727-770): ambient += indirect, final gather, caustics; clamp to sqrt(3)
+__global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, const NodeRec* __restrict__ rec, int64_t n,
+                                                     const double* __restrict__ gi_extra,
+                                                     const double* __restrict__ fgather, double* __restrict__ surface) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeRec& nr = rec[i];
+    if (nr.material < 0 || !any_positive(nr.Kd)) return;
+    double* a = surface + 12 * i;
+    for (int k = 0; k < 3; ++k) a[k] += gi_extra[6 * i + k];
+    if (fgather != nullptr)
+        for (int k = 0; k < 3; ++k) a[k] += fgather[3 * i + k];
+    for (int k = 0; k < 3; ++k) a[k] += gi_extra[6 * i + 3 + k];
+    const double len = a[0] + a[1] + a[2];
+    if (len > 1.7320508075688772) {
+        for (int k = 0; k < 3; ++k) a[k] *= 1.0 / len;
+        for (int k = 0; k < 3; ++k) a[k] *= 1.7320508075688772;
+    }
+}
+
 }  // namespace frt
 
 // ======================================================================
@@ -659,6 +1009,28 @@ struct frt_scene_handle {
     std::vector<hipEvent_t> ev_pool;
     std::vector<Mark> ev_marks;
     size_t ev_used = 0;
+    // global illumination: photon maps (traced per render seed) and work buffers
+    std::vector<frt_light> host_lights;
+    struct Gi {
+        bool built = false;
+        uint64_t seed = 0;
+        void* map_mem[2] = {nullptr, nullptr};  // one allocation per map: pos | power | dir | start
+        uint64_t photons[2] = {0, 0};
+        frt::QueuedRay* pq[2] = {nullptr, nullptr};
+        double* ppow[2] = {nullptr, nullptr};
+        int64_t pq_cap[2] = {0, 0}, ppow_cap[2] = {0, 0};
+        frt::HitRec* phits = nullptr;
+        int64_t phits_cap = 0;
+        frt::StoredPhoton* store = nullptr;
+        int64_t store_cap = 0;
+        frt::QueuedRay* gq = nullptr;
+        frt::HitRec* ghits = nullptr;
+        double* gcol = nullptr;
+        int64_t gq_cap = 0, ghits_cap = 0, gcol_cap = 0;
+        double* extra = nullptr;
+        double* fgather = nullptr;
+        int64_t extra_cap = 0, fgather_cap = 0;
+    } gi;
 };
 
 static thread_local std::string g_last_error;
@@ -889,6 +1261,11 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     S.num_patterns = sc->num_patterns;
     S.cam = sc->camera;
     S.cfg = sc->config;
+    h->host_lights.assign(sc->lights, sc->lights + sc->num_lights);
+    if (S.cfg.use_gi && (S.cfg.gi_path_length >= 255 || S.cfg.photon_count <= 0)) {
+        frt_scene_release(h);
+        return fail("frt_scene_upload: global illumination needs photon maps (photon_count > 0) and path_length < 255");
+    }
 
     std::vector<int32_t> jl, jp;
     for (int l = 0; l < sc->num_lights; ++l)
@@ -936,6 +1313,21 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(L.counts));
     }
     hip_ignore(hipFree(h->hits));
+    {
+        auto& G = h->gi;
+        for (int m = 0; m < 2; ++m) {
+            hip_ignore(hipFree(G.map_mem[m]));
+            hip_ignore(hipFree(G.pq[m]));
+            hip_ignore(hipFree(G.ppow[m]));
+        }
+        hip_ignore(hipFree(G.phits));
+        hip_ignore(hipFree(G.store));
+        hip_ignore(hipFree(G.gq));
+        hip_ignore(hipFree(G.ghits));
+        hip_ignore(hipFree(G.gcol));
+        hip_ignore(hipFree(G.extra));
+        hip_ignore(hipFree(G.fgather));
+    }
     hip_ignore(hipFree(h->sample_col));
     hip_ignore(hipFree(h->out_dev));
     hip_ignore(hipFree(h->counters));
@@ -1021,17 +1413,20 @@ static void collect_timings(frt_scene_handle* h, frt_frame_stats* st) {
 // scene-specialised traversal kernels: the template instance without CSG
 // frames / the quartic keeps register pressure down for scenes that lack them
 template <int F>
-static void launch_trace_f(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n) {
+static void launch_trace_f(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
+                           frt::HitRec* hits, int filter_casts) {
     hipLaunchKernelGGL(frt::k_trace<F>, dim3(grid_for(n, frt::kTraceBlock)), dim3(frt::kTraceBlock), h->lds_bytes,
-                       h->stream, h->S, B, q, n, h->hits, h->err);
+                       h->stream, h->S, B, q, n, hits, h->err, filter_casts);
 }
 
-static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n) {
+static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
+                         frt::HitRec* hits = nullptr, int filter_casts = 0) {
+    if (hits == nullptr) hits = h->hits;
     switch (h->S.features & 3) {
-    case 0: launch_trace_f<0>(h, B, q, n); break;
-    case 1: launch_trace_f<1>(h, B, q, n); break;
-    case 2: launch_trace_f<2>(h, B, q, n); break;
-    default: launch_trace_f<3>(h, B, q, n); break;
+    case 0: launch_trace_f<0>(h, B, q, n, hits, filter_casts); break;
+    case 1: launch_trace_f<1>(h, B, q, n, hits, filter_casts); break;
+    case 2: launch_trace_f<2>(h, B, q, n, hits, filter_casts); break;
+    default: launch_trace_f<3>(h, B, q, n, hits, filter_casts); break;
     }
 }
 
@@ -1049,6 +1444,229 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
     case 2: launch_shadow_f<2>(h, B, rec, n, counts); break;
     default: launch_shadow_f<3>(h, B, rec, n, counts); break;
     }
+}
+
+
+// ---------------------------------------------------------------------
+// photon maps (reference photon_tracer.c:203-257, pm.c)
+// ---------------------------------------------------------------------
+
+static uint64_t host_mix64(uint64_t x) {  // frt::mix64 on the host
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31;
+    return x;
+}
+
+// Photons of one light into one map, in the reference's storage order: emission
+// by emission (each emission's stores in bounce order) until the stored count
+// reaches the light's share, the last emission kept whole (trace_photons'
+// "j += hit" loop). Emissions run in batches on the device; the batch size
+// follows the measured store rate. The reference loops forever when a light
+// can store nothing (no diffuse surface reachable); here the emission count is
+// bounded and the map keeps what was found.
+static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t seed,
+                               std::vector<frt::StoredPhoton>& out) {
+    using namespace frt;
+    auto& G = h->gi;
+    const int64_t want = h->host_lights[(size_t)light].num_photons;
+    const int path = h->S.cfg.gi_path_length;
+    if (want <= 0 || path <= 0) return 0;
+    const int64_t kMaxBatch = (int64_t)1 << 22;
+    const uint64_t emit_limit = (uint64_t)want * 4096ull + ((uint64_t)1 << 26);
+    const uint64_t lseed = host_mix64(seed ^ host_mix64(0x70686f746f6e0000ULL + (uint64_t)(map * 4096 + light)));
+    std::vector<StoredPhoton> acc;
+    uint64_t e0 = 0;
+    int64_t batch = std::min<int64_t>(std::max<int64_t>(want, 4096), kMaxBatch);
+    Batch B{};
+    B.seed = seed;
+    for (;;) {
+        const int64_t store_cap = batch * (int64_t)std::min(path, 16);
+        if (grow(&G.pq[0], G.pq_cap[0], batch) || grow(&G.pq[1], G.pq_cap[1], batch) ||
+            grow(&G.ppow[0], G.ppow_cap[0], 3 * batch) || grow(&G.ppow[1], G.ppow_cap[1], 3 * batch) ||
+            grow(&G.phits, G.phits_cap, batch) || grow(&G.store, G.store_cap, store_cap))
+            return -1;
+        unsigned long long* store_count = h->counters + 24;
+        unsigned long long* next_count = h->counters + 25;
+        FRT_HIP(hipMemsetAsync(h->counters + 24, 0, 2 * sizeof(unsigned long long), h->stream));
+        hipLaunchKernelGGL(k_photon_emit, dim3(grid_for(batch)), dim3(kBlock), 0, h->stream, h->S, lseed, light, e0,
+                           batch, G.pq[0], G.ppow[0]);
+        FRT_HIP(hipGetLastError());
+        int64_t n = batch;
+        int cur = 0;
+        for (int depth = 0; depth < path && n > 0; ++depth) {
+            FRT_HIP(hipMemsetAsync(next_count, 0, sizeof(unsigned long long), h->stream));
+            launch_trace(h, B, G.pq[cur], n, G.phits, 1);
+            FRT_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_photon_hit, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, lseed, map, depth,
+                               G.pq[cur], G.ppow[cur], n, G.phits, G.pq[cur ^ 1], G.ppow[cur ^ 1], next_count,
+                               batch, G.store, store_count, store_cap, h->err);
+            FRT_HIP(hipGetLastError());
+            unsigned long long nn = 0;
+            FRT_HIP(hipMemcpyAsync(&nn, next_count, sizeof(nn), hipMemcpyDeviceToHost, h->stream));
+            FRT_HIP(hipStreamSynchronize(h->stream));
+            n = (int64_t)std::min<unsigned long long>(nn, (unsigned long long)batch);
+            cur ^= 1;
+        }
+        unsigned long long ns = 0;
+        FRT_HIP(hipMemcpyAsync(&ns, store_count, sizeof(ns), hipMemcpyDeviceToHost, h->stream));
+        FRT_HIP(hipStreamSynchronize(h->stream));
+        ns = std::min<unsigned long long>(ns, (unsigned long long)store_cap);
+        const size_t base = acc.size();
+        acc.resize(base + (size_t)ns);
+        if (ns) FRT_HIP(hipMemcpy(acc.data() + base, G.store, (size_t)ns * sizeof(StoredPhoton), hipMemcpyDeviceToHost));
+        e0 += (uint64_t)batch;
+        if ((int64_t)acc.size() >= want || e0 >= emit_limit) break;
+        const double rate = (double)acc.size() / (double)e0;
+        const double need = (double)(want - (int64_t)acc.size());
+        batch = rate > 0 ? (int64_t)std::min<double>((double)kMaxBatch, need / rate * 1.25 + 1024.0)
+                         : std::min<int64_t>(batch * 4, kMaxBatch);
+    }
+    std::sort(acc.begin(), acc.end(), [](const StoredPhoton& a, const StoredPhoton& b) { return a.key < b.key; });
+    // keep the emissions up to the first one at which the count reaches `want`
+    size_t keep = acc.size();
+    if ((int64_t)acc.size() >= want) {
+        const uint64_t last = acc[(size_t)want - 1].key >> 8;
+        keep = (size_t)want;
+        while (keep < acc.size() && (acc[keep].key >> 8) == last) ++keep;
+    }
+    out.insert(out.end(), acc.begin(), acc.begin() + (ptrdiff_t)keep);
+    return 0;
+}
+
+// pm_store's direction bytes decoded by pm_photon_dir (pm.c:80-88, 288-300)
+static void quantized_dir(const double* d, double* out) {
+    double at = std::acos(d[2]) * (256.0 / M_PI);
+    int theta = std::isfinite(at) ? (int)at : 0;
+    theta = theta > 255 ? 255 : theta;
+    double ap = std::atan2(d[1], d[0]) * (256.0 / (2.0 * M_PI));
+    int phi = std::isfinite(ap) ? (int)ap : 0;
+    phi = phi > 255 ? 255 : (phi < 0 ? phi + 256 : phi);
+    theta &= 255;
+    phi &= 255;
+    const double ta = (double)theta * (1.0 / 256.0) * M_PI, pa = (double)phi * (1.0 / 256.0) * M_PI;
+    out[0] = std::sin(ta) * std::cos(2.0 * pa);
+    out[1] = std::sin(ta) * std::sin(2.0 * pa);
+    out[2] = std::cos(ta);
+}
+
+// hashed uniform grid over the photons (frt_gi.hpp for_photons_within): one
+// allocation per map, photons sorted by bucket
+static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::StoredPhoton>& ph, double scale) {
+    auto& G = h->gi;
+    hip_ignore(hipFree(G.map_mem[m]));
+    G.map_mem[m] = nullptr;
+    frt::PhotonMapDev M{};
+    const int64_t n = (int64_t)ph.size();
+    M.count = n;
+    M.cell = h->S.cfg.irradiance_radius > 0 ? h->S.cfg.irradiance_radius : 1.0;
+    int64_t nb = 1;
+    while (nb < 2 * n) nb <<= 1;
+    if (nb > ((int64_t)1 << 30) || n > ((int64_t)1 << 30)) return fail("photon map too large");
+    M.num_buckets = (int32_t)nb;
+    for (int k = 0; k < 3; ++k) M.origin[k] = 0.0;
+    if (n > 0)
+        for (int k = 0; k < 3; ++k) {
+            double lo = ph[0].pos[k];
+            for (const auto& p : ph) lo = std::min(lo, p.pos[k]);
+            M.origin[k] = std::isfinite(lo) ? lo : 0.0;
+        }
+    std::vector<uint32_t> bucket((size_t)n);
+    std::vector<int32_t> start((size_t)nb + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t c[3];
+        for (int k = 0; k < 3; ++k) c[k] = (int64_t)std::floor((ph[(size_t)i].pos[k] - M.origin[k]) / M.cell);
+        const uint64_t hsh = (uint64_t)c[0] * 73856093ull ^ (uint64_t)c[1] * 19349663ull ^ (uint64_t)c[2] * 83492791ull;
+        bucket[(size_t)i] = (uint32_t)(host_mix64(hsh) & (uint64_t)(nb - 1));
+        start[bucket[(size_t)i] + 1]++;
+    }
+    for (int64_t b = 0; b < nb; ++b) start[(size_t)b + 1] += start[(size_t)b];
+    std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    const size_t nd = (size_t)std::max<int64_t>(n, 1) * 9;
+    std::vector<double> data(nd, 0.0);
+    double* pos = data.data();
+    double* pow = pos + 3 * std::max<int64_t>(n, 1);
+    double* dir = pow + 3 * std::max<int64_t>(n, 1);
+    for (int64_t i = 0; i < n; ++i) {
+        const auto& p = ph[(size_t)i];
+        const int64_t j = fill[bucket[(size_t)i]]++;
+        double d[3];
+        quantized_dir(p.dir, d);
+        for (int k = 0; k < 3; ++k) {
+            pos[3 * j + k] = p.pos[k];
+            pow[3 * j + k] = p.power[k] * scale;  // pm_scale_photon_power
+            dir[3 * j + k] = d[k];
+        }
+    }
+    const size_t bytes = nd * sizeof(double) + start.size() * sizeof(int32_t);
+    FRT_HIP(hipMalloc(&G.map_mem[m], bytes));
+    FRT_HIP(hipMemcpy(G.map_mem[m], data.data(), nd * sizeof(double), hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy((char*)G.map_mem[m] + nd * sizeof(double), start.data(), start.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
+    const double* base = (const double*)G.map_mem[m];
+    M.pos = base;
+    M.power = base + 3 * std::max<int64_t>(n, 1);
+    M.dir = base + 6 * std::max<int64_t>(n, 1);
+    M.start = (const int32_t*)((const char*)G.map_mem[m] + nd * sizeof(double));
+    h->S.pmaps[m] = M;
+    G.photons[m] = (uint64_t)n;
+    return 0;
+}
+
+// trace_photons for one render seed: caustic map 0, global map 1
+static int build_photon_maps(frt_scene_handle* h, uint64_t seed) {
+    const auto& cfg = h->S.cfg;
+    const int want[2] = {cfg.trace_caustic_map, cfg.trace_global_map};
+    for (int m = 0; m < 2; ++m) {
+        std::vector<frt::StoredPhoton> ph;
+        if (want[m])
+            for (int l = 0; l < h->S.num_lights; ++l)
+                if (trace_light_photons(h, m, l, seed, ph)) return -1;
+        // pm_store keeps at most max_photons + 1 photons (pm.c:271)
+        if ((int64_t)ph.size() > cfg.photon_count + 1) ph.resize((size_t)cfg.photon_count + 1);
+        if (build_photon_map(h, m, ph, 1.0 / (double)cfg.photon_count)) return -1;
+    }
+    h->gi.built = true;
+    h->gi.seed = seed;
+    return 0;
+}
+
+// shade_hit's GI terms for the nodes of one level (renderer.c:727-770); chunks of
+// nodes keep the final-gather queue bounded
+static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::Level& L, int64_t n, frt_frame_stats* st) {
+    using namespace frt;
+    auto& G = h->gi;
+    const auto& cfg = h->S.cfg;
+    if (grow(&G.extra, G.extra_cap, 6 * n) || grow(&G.fgather, G.fgather_cap, 3 * n)) return -1;
+    hipLaunchKernelGGL(k_gi_node, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, L.rec, n, G.extra);
+    FRT_HIP(hipGetLastError());
+    const int64_t rays_per = (int64_t)cfg.gi_usteps * (int64_t)cfg.gi_vsteps;
+    const bool gather = cfg.include_final_gather && rays_per > 0;
+    if (gather) {
+        const int64_t kChunkRays = (int64_t)1 << 22;
+        const int64_t chunk = std::max<int64_t>(1, kChunkRays / rays_per);
+        for (int64_t n0 = 0; n0 < n; n0 += chunk) {
+            const int64_t m = std::min(chunk, n - n0);
+            const int64_t rays = m * rays_per;
+            if (grow(&G.gq, G.gq_cap, rays) || grow(&G.ghits, G.ghits_cap, rays) || grow(&G.gcol, G.gcol_cap, 3 * rays))
+                return -1;
+            hipLaunchKernelGGL(k_gather_gen, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, L.rec, n0, m,
+                               G.gq);
+            launch_trace(h, B, G.gq, rays, G.ghits, 0);
+            hipLaunchKernelGGL(k_gather_shade, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq,
+                               G.ghits, rays, G.gcol);
+            hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
+                               G.fgather);
+            FRT_HIP(hipGetLastError());
+            if (st) st->gather_rays += (uint64_t)rays;
+        }
+    }
+    hipLaunchKernelGGL(k_gi_apply, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, L.rec, n, G.extra,
+                       gather ? G.fgather : nullptr, L.surface);
+    FRT_HIP(hipGetLastError());
+    return 0;
 }
 
 extern "C" {
@@ -1087,6 +1705,30 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
     }
     FRT_HIP(hipMemsetAsync(h->err, 0, sizeof(unsigned), h->stream));
     FRT_HIP(hipMemsetAsync(h->counters, 0, 32 * sizeof(unsigned long long), h->stream));
+    if (h->S.cfg.use_gi && (!h->gi.built || h->gi.seed != P->seed)) {
+        // the photon maps belong to the render seed: same seed, same image (also across row splits)
+        hipEvent_t p0 = nullptr, p1 = nullptr;
+        if (st) {
+            hip_ignore(hipEventCreate(&p0));
+            hip_ignore(hipEventCreate(&p1));
+            hip_ignore(hipEventRecord(p0, h->stream));
+        }
+        const int rc = build_photon_maps(h, P->seed);
+        if (st) {
+            hip_ignore(hipEventRecord(p1, h->stream));
+            hip_ignore(hipEventSynchronize(p1));
+            float ms = 0.f;
+            hip_ignore(hipEventElapsedTime(&ms, p0, p1));
+            st->photon_ms = ms;
+            hip_ignore(hipEventDestroy(p0));
+            hip_ignore(hipEventDestroy(p1));
+        }
+        if (rc) return rc;
+    }
+    if (st) {
+        st->photons[0] = h->gi.photons[0];
+        st->photons[1] = h->gi.photons[1];
+    }
     unsigned long long host_counters[32];
     for (int64_t p0 = 0; p0 < npix; p0 += pix_per_batch) {
         const int64_t bp = std::min<int64_t>(pix_per_batch, npix - p0);
@@ -1140,6 +1782,10 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
                 hipLaunchKernelGGL(k_shade, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n, L.counts,
                                    L.surface);
                 FRT_HIP(hipGetLastError());
+            }
+            if (h->S.cfg.use_gi) {
+                KTimer t(h, st, 7);
+                if (shade_gi(h, B, L, n, st)) return -1;
             }
             FRT_HIP(hipMemcpyAsync(host_counters, h->counters, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                    h->stream));

@@ -65,6 +65,19 @@ __device__ __forceinline__ void frame_cache(const Ray& r, FrameCache& c) {
     c.dmax = fmaxf(fmaxf(fabsf(c.df[0]), fabsf(c.df[1])), fabsf(c.df[2]));
 }
 
+// one photon map (frt_gi.hpp): photons sorted by grid bucket (SoA), built on the host after tracing
+struct PhotonMapDev {
+    const double* pos;    // 3 per photon
+    const double* power;  // 3 per photon (scaled by 1 / photon_count)
+    const double* dir;    // 3 per photon: pm_photon_dir of the stored theta / phi bytes (pm.c:80-88)
+    const int32_t* start; // bucket -> first photon, num_buckets + 1 entries
+    int64_t count;
+    int32_t num_buckets;  // power of two
+    int32_t pad;
+    double origin[3];     // grid origin
+    double cell;          // cell edge = the estimate's radius
+};
+
 struct DevScene {
     const WalkNode* __restrict__ wn;
     const frt_node* __restrict__ nodes;
@@ -89,6 +102,7 @@ struct DevScene {
     int32_t walk_flags;       // FRT_WALK_FLAGS (A/B experiments): bit0 no prefilter, bit1 exact box decisions, bit2 exact cubes
     frt_camera cam;
     frt_config cfg;
+    PhotonMapDev pmaps[2];  // 0 caustic, 1 global (global illumination only)
 };
 
 enum FeatureBits : int { kFeatCsg = 1, kFeatTorus = 2 };
@@ -265,7 +279,9 @@ __device__ __forceinline__ double node_ni(const DevScene& S, int node) {
 
 template <bool kShadow, int kFeat>
 __device__ int walk(const DevScene& S, const Ray& world, double distance, bool live, double& best_t, char* smem,
-                    unsigned& err, double* n12 = nullptr) {
+                    unsigned& err, double* n12 = nullptr, bool filter_casts = false) {
+    // filter_casts (closest hit only): hit(xs, true) of the photon tracer (photon_tracer.c:185),
+    // the first positive entry whose material casts shadows
     constexpr bool kCsg = (kFeat & kFeatCsg) != 0;
     constexpr bool kTorus = (kFeat & kFeatTorus) != 0;
     constexpr int kNone = 0x7fffffff;
@@ -338,7 +354,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                             int unit_best = -1;
                             for (int k = 0; k < n; ++k) {
                                 const double t = W.T(k);
-                                if (t > 0 && (best < 0 || t < best_t)) {
+                                if (t > 0 && (best < 0 || t < best_t) && (!filter_casts || S.casts[W.N(k)])) {
                                     best_t = t;
                                     best = W.N(k);
                                     unit_best = best;
@@ -532,7 +548,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const double t = H.t.at(j);
-                        if (j < H.t.n && t > 0 && (best < 0 || t < best_t)) {
+                        if (j < H.t.n && t > 0 && (best < 0 || t < best_t) && (!filter_casts || nd.casts)) {
                             best_t = t;
                             best = i;
                             took = true;

@@ -445,6 +445,21 @@ frt_flatten_scene(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter
         }
         fl->num_samples = (int32_t)l->num_samples;
         fl->rows = (int32_t)l->surface_points_cache_len;
+        /* photon emission data (light.c:14-99) */
+        if (l->type == AREA_LIGHT) {
+            Vector tmp;
+            vector_cross((double *)l->u.area.uvec, (double *)l->u.area.vvec, tmp);
+            Vector nrm;
+            vector_normalize(tmp, nrm);
+            memcpy(fl->normal, nrm, 3 * sizeof(double));
+        } else if (l->type == CIRCLE_LIGHT) {
+            memcpy(fl->normal, l->u.circle.normal, 3 * sizeof(double));
+        } else if (l->type == HEMISPHERE_LIGHT) {
+            memcpy(fl->normal, l->u.hemi.normal, 3 * sizeof(double));
+            memcpy(fl->position, l->u.hemi.position, 3 * sizeof(double));
+        } else {
+            memcpy(fl->position, frt_light_position(l), 3 * sizeof(double));
+        }
         fl->points = (int64_t)(3 * at);
         memcpy(fl->intensity, l->intensity, 3 * sizeof(double));
         for (size_t r = 0; r < l->surface_points_cache_len; ++r) {
@@ -501,6 +516,35 @@ frt_flatten_scene(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter
     out->config.include_specular = ic->di.include_specular;
     out->config.path_length = (int32_t)ic->di.path_length;
     out->config.all_ni_one = c.all_ni_one;
+    /* global illumination (renderer.c:52-71: use_gi = include_global || visualize_photon_map) */
+    out->config.use_gi = (ic->include_global || ic->debug_visualize_photon_map) ? 1 : 0;
+    out->config.visualize_photon_map = ic->debug_visualize_photon_map ? 1 : 0;
+    out->config.include_caustics = ic->gi.include_caustics ? 1 : 0;
+    out->config.include_final_gather = ic->gi.include_final_gather ? 1 : 0;
+    out->config.gi_usteps = (int32_t)ic->gi.usteps;
+    out->config.gi_vsteps = (int32_t)ic->gi.vsteps;
+    out->config.irradiance_num = (int32_t)ic->gi.irradiance_estimate_num;
+    out->config.gi_path_length = (int32_t)ic->gi.path_length;
+    out->config.irradiance_radius = ic->gi.irradiance_estimate_radius;
+    out->config.cone_filter_k = ic->gi.irradiance_estimate_cone_filter_k;
+    if (w->photon_maps != NULL && w->frt_photons_requested) {
+        out->config.photon_count = (int64_t)w->photon_maps->max_photons;
+        out->config.trace_caustic_map = w->frt_trace_caustic;
+        out->config.trace_global_map = w->frt_trace_global;
+    }
+    /* apportion the photons by CIE L* of each light's intensity (photon_tracer.c:202-215) */
+    if (out->config.photon_count > 0 && w->lights_num > 0) {
+        double total_lightness = 0.0;
+        Color lab;
+        for (size_t i = 0; i < w->lights_num; ++i) {
+            rgb_to_lab(w->lights[i].intensity, lab);
+            total_lightness += lab[0];
+        }
+        for (size_t i = 0; i < w->lights_num; ++i) {
+            rgb_to_lab(w->lights[i].intensity, lab);
+            lights[i].num_photons = (int64_t)(size_t)((double)(size_t)out->config.photon_count * lab[0] / total_lightness);
+        }
+    }
 
     pm_free(&c.mat_map);
     pm_free(&c.pat_map);

@@ -3,10 +3,8 @@
  *
  * world() mirrors reference src/renderer/world.c:14-28. The photon-map
  * storage API (pm.h) keeps the reference's struct so generated main() can
- * allocate maps; photon tracing and the GPU radiance estimate are the next
- * hot-path row and render_multi refuses
- * global-illumination configs until they land, rather than silently
- * rendering something different.
+ * allocate maps; trace_photons() records the request and render_multi traces
+ * the photons on the GPU (frt_gi.hpp).
  */
 #include <math.h>
 #include <stdio.h>
@@ -105,11 +103,14 @@ pm_balance(PhotonMap *pm)
 void
 trace_photons(const World w, const size_t num_photons, bool include_caustics, bool include_final_gather)
 {
-    (void)w;
+    /* Reference photon_tracer.c:195-245 traces here, on the CPU. frt records the
+     * request; render_multi traces the photons on the GPU after the scene upload
+     * (fast_ray_tracer_amd/csrc/frt_gi.hpp), then balances the maps on the host. */
     (void)num_photons;
-    (void)include_caustics;
-    (void)include_final_gather;
-    fprintf(stderr,
-            "frt: photon tracing (global illumination) is not implemented in this build; "
-            "render_multi will refuse include-global scenes\n");
+    if (w == NULL) {
+        return;
+    }
+    w->frt_photons_requested = 1;
+    w->frt_trace_caustic = include_caustics ? 1 : 0;
+    w->frt_trace_global = include_final_gather ? 1 : 0;
 }

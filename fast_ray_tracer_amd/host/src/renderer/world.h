@@ -19,6 +19,9 @@ typedef struct world {
     size_t shapes_num;
     PhotonMap *photon_maps;
     Global_config global_config;
+    /* frt: trace_photons() records its request here; the photons are traced on the GPU by render_multi */
+    int frt_photons_requested;
+    int frt_trace_caustic, frt_trace_global;
 } *World;
 
 World world(void);

@@ -33,15 +33,18 @@ class FrameStats(ctypes.Structure):
                 ("shadow_rays", ctypes.c_uint64), ("pruned_secondary", ctypes.c_uint64),
                 ("hits", ctypes.c_uint64), ("errors", ctypes.c_uint64), ("render_ms", ctypes.c_double),
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_uint64 * 8),
-                ("shadow_kernel_bytes", ctypes.c_double)]
+                ("shadow_kernel_bytes", ctypes.c_double), ("gather_rays", ctypes.c_uint64),
+                ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
-        names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "k7"]
+        names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
             "hits": int(self.hits), "errors": int(self.errors), "render_ms": float(self.render_ms),
             "shadow_kernel_bytes": float(self.shadow_kernel_bytes),
+            "gather_rays": int(self.gather_rays), "photons": [int(self.photons[0]), int(self.photons[1])],
+            "photon_ms": float(self.photon_ms),
             "kernel_ms": {names[i]: float(self.kernel_ms[i]) for i in range(8) if self.kernel_launches[i]},
             "kernel_launches": {names[i]: int(self.kernel_launches[i]) for i in range(8) if self.kernel_launches[i]},
         }

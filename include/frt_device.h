@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 1u
+#define FRT_ABI_VERSION 2u
 
 /* node kinds: same numbering as the reference's enum shape_enum (shapes.h:16-27) */
 enum frt_node_type {
@@ -120,6 +120,10 @@ typedef struct frt_light {
     int32_t pad;
     int64_t points;      /* offset into frt_scene.light_points (3 doubles per point, row-major) */
     double intensity[3];
+    /* photon emission (reference light.c:14-99, photon_tracer.c:195-233) */
+    double normal[3];    /* emission hemisphere axis: area normalize(uvec x vvec), circle / hemisphere normal */
+    double position[3];  /* point / hemisphere light position */
+    int64_t num_photons; /* photons apportioned to this light by CIE L* (trace_photons) */
 } frt_light;
 
 typedef struct frt_camera {
@@ -137,6 +141,19 @@ typedef struct frt_config {
     int32_t path_length;
     int32_t all_ni_one;      /* every material has Ni == 1.0: n1 = n2 = 1 without the container walk */
     int32_t pad;
+    /* global illumination (reference renderer.c:52-71, photon_tracer.c, pm.c) */
+    int32_t use_gi;                 /* include_global || debug_visualize_photon_map */
+    int32_t visualize_photon_map;
+    int32_t include_caustics;       /* gi.include_caustics */
+    int32_t include_final_gather;   /* gi.include_final_gather */
+    int32_t gi_usteps, gi_vsteps;   /* final-gather hemisphere grid */
+    int32_t irradiance_num;         /* k of the k-nearest-photon estimate */
+    int32_t gi_path_length;         /* photon bounces */
+    int32_t trace_caustic_map;      /* trace_photons(populate_caustic_map, ...) */
+    int32_t trace_global_map;       /* trace_photons(..., populate_global_map) */
+    int64_t photon_count;           /* photons per map (gi.photon_count); 0: no maps */
+    double irradiance_radius;
+    double cone_filter_k;
 } frt_config;
 
 typedef struct frt_scene {
@@ -189,9 +206,12 @@ typedef struct frt_frame_stats {
     uint64_t hits;                /* path nodes shaded */
     uint64_t errors;              /* capacity / depth overflows (non-zero = result invalid) */
     double render_ms;             /* wall time of the device work (events) */
-    double kernel_ms[8];          /* per-kernel accumulated time: trace, shadow, shade, combine, resolve, trace (level 0), prepare */
+    double kernel_ms[8];          /* per-kernel accumulated time: trace, shadow, shade, combine, resolve, trace (level 0), prepare, gi */
     uint64_t kernel_launches[8];
     double shadow_kernel_bytes;   /* algorithmic bytes moved by the shadow kernel (DESIGN.md byte model) */
+    uint64_t gather_rays;         /* final-gather rays traced (global illumination) */
+    uint64_t photons[2];          /* photons in the caustic / global map used by this frame */
+    double photon_ms;             /* photon tracing + map build of this frame (0 when the maps were reused) */
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */

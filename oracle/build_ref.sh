@@ -7,7 +7,7 @@
 #
 # produces oracle/_ref/bin/<name>: the reference library objects + the given
 # codegen output (yaml_parser.py scene.yml > main.c) + oracle/ref_harness.c,
-# with main.c's render_multi call routed through frt_ref_render_multi so the
+# with main.c's render_multi / trace_photons calls routed through the harness so the
 # raw canvas and the render_multi wall time can be captured
 # (FRT_REF_CANVAS=<file>, FRT_REF_STATS=<file>). Used to pin the CPU oracle
 # (tests/golden/make_golden.py) and as bench.py's cpu_baseline ("reference").
@@ -51,7 +51,7 @@ if [ ! -f "$harness" ] || [ "$HERE/ref_harness.c" -nt "$harness" ]; then
     "$CC" "${CFLAGS[@]}" -I"$REF" -c "$HERE/ref_harness.c" -o "$harness"
 fi
 
-"$CC" "${CFLAGS[@]}" -I"$REF" -Drender_multi=frt_ref_render_multi \
+"$CC" "${CFLAGS[@]}" -I"$REF" -Drender_multi=frt_ref_render_multi -Dtrace_photons=frt_ref_trace_photons \
     -c "$MAIN" -o "$OUT/obj/main_$NAME.o"
 "$CC" -o "$OUT/bin/$NAME" "$OUT/obj/main_$NAME.o" "$harness" "${objs[@]}" "${LDFLAGS[@]}"
 echo "$OUT/bin/$NAME"

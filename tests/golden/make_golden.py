@@ -74,9 +74,24 @@ SCENES = {
     "cornell_shipped_48_4x4": ("scenes/cornell_box/cornell_box.yml",
                                {"size": (48, 48), "steps": (4, 4), "jitter": True, "gi_off": True, "threads": 1,
                                 "extra_seeds": STOCHASTIC_SEEDS}),
-    # global illumination (photon map + final gather) as shipped: main.c only, the input of the
-    # "unsupported features fail loudly" test (no device path yet)
+    # global illumination (photon maps + final gather): the shipped configuration (1M photons,
+    # 8x8 gather, k = 200) at 16x16 (main.c only), and statistical goldens: the shipped GI at 24x24,
+    # the raw global-map estimate (visualize-photon-map) and the caustic map alone
     "cornell_gi_16": ("scenes/cornell_box/cornell_box.yml", {"size": (16, 16), "no_golden": True}),
+    # include-global with photon-count 0: the reference dereferences a NULL photon map; the
+    # drop-in refuses it (test_unimplemented_features_fail_loudly)
+    "cornell_gi_nomaps_16": ("scenes/cornell_box/cornell_box.yml",
+                             {"size": (16, 16), "no_golden": True, "gi": {"photon-count": 0}}),
+    "cornell_gi_24": ("scenes/cornell_box/cornell_box.yml",
+                      {"size": (24, 24), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS, "gi": {}}),
+    "cornell_gi_visualize_32": ("scenes/cornell_box/cornell_box.yml",
+                                {"size": (32, 32), "steps": (2, 2), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS,
+                                 "ill": {"visualize-photon-map": True},
+                                 "gi": {"usteps": 2, "vsteps": 2, "photon-count": 200000}}),
+    "cornell_caustics_32": ("scenes/cornell_box/cornell_box.yml",
+                            {"size": (32, 32), "steps": (2, 2), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS,
+                             "gi": {"include-caustics": True, "include-final-gather": False,
+                                    "photon-count": 100000}}),
     "checkered_sphere_dof_100": ("scenes/checkered_sphere/checkered_sphere.yml",
                                  {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
                                   "aperture": (["CIRCULAR_APERTURE", 1.0], 0.4), "extra_seeds": STOCHASTIC_SEEDS}),
@@ -122,6 +137,10 @@ def apply_overrides(tree, name, ov):
     cfg = cfgs[0]
     cfg.setdefault("threading", {})["thread-count"] = ov.get("threads", 8)
     cfg.setdefault("output", {})["file"] = os.path.join(SCRATCH, "out", name)
+    if "ill" in ov:
+        cfg.setdefault("illumination", {}).update(ov["ill"])
+    if "gi" in ov:
+        cfg.setdefault("illumination", {}).setdefault("global-illumination", {}).update(ov["gi"])
     if ov.get("gi_off"):
         ill = cfg.setdefault("illumination", {})
         ill["include-global"] = False
@@ -224,6 +243,8 @@ def main(names):
                 extra.append(np.fromfile(canvas_bin, dtype=np.float64).reshape(h, w, 4)[:, :, :3])
             arrays["refs"] = np.stack([canvas] + extra)
             entry["stochastic"] = True
+            if "gi" in ov:
+                entry["gi"] = True  # photon maps: statistical parity against the reference renders only
             entry["extra_seeds"] = list(ov["extra_seeds"])
         if not ov.get("hash_only"):
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)

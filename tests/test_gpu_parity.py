@@ -45,9 +45,10 @@ def test_gpu_matches_reference_canvas_and_ppm(built, name):
 
 
 def test_unimplemented_features_fail_loudly(built):
-    """Features without a device path are refused at upload with the reason, never rendered wrong."""
+    """Configurations the reference cannot render are refused at upload with the reason, never
+    rendered wrong: global illumination with photon-count 0 (the reference reads a NULL photon map)."""
     from fast_ray_tracer_amd.runtime import GpuRenderer
-    scene = load_scene("cornell_gi_16")  # cornell_box as shipped: include-global (photon map)
+    scene = load_scene("cornell_gi_nomaps_16")
     with pytest.raises(RuntimeError, match="not (supported|implemented)"):
         GpuRenderer(scene)
 

@@ -67,10 +67,12 @@ def test_gpu_stochastic_paths_match_reference_distribution(built, name):
     assert abs(bias) <= tol
 
 
-def test_gpu_stochastic_seeding(built):
-    """Same seed -> identical image; another seed -> another sample; row splits stay exact."""
+@pytest.mark.parametrize("name", ["checkered_sphere_dof_100", "cornell_caustics_32"])
+def test_gpu_stochastic_seeding(built, name):
+    """Same seed -> identical image; another seed -> another sample; row splits stay exact
+    (photon maps belong to the seed, so they too are reproduced per seed)."""
     from fast_ray_tracer_amd.runtime import GpuRenderer
-    r = GpuRenderer(load_scene("checkered_sphere_dof_100"))
+    r = GpuRenderer(load_scene(name))
     a = r.render(seed=1)
     assert np.array_equal(a, r.render(seed=1))
     assert not np.array_equal(a, r.render(seed=2))

@@ -14,8 +14,10 @@ import pytest
 from conftest import canvas_goldens, fresh_scene, golden_index, load_golden_canvas, load_scene
 
 
-@pytest.mark.parametrize("name", canvas_goldens())
+@pytest.mark.parametrize("name", [n for n in canvas_goldens() if not golden_index()[n].get("gi")])
 def test_oracle_matches_reference_bit_exact(built, name):
+    """(Global-illumination goldens are checked statistically on the GPU only: the oracle
+    restates the direct / recursive path, not the photon tracer.)"""
     import oracle
     stochastic = bool(golden_index()[name].get("stochastic"))
     # stochastic goldens (drand48 jitter / apertures, rand() light-cache rows) were rendered by the
