@@ -33,7 +33,9 @@
 #include <vector>
 
 #include "frt_device.h"
+#include "frt_jit.h"
 #include "frt_shade.hpp"
+#include "frt_shadow.hpp"
 
 namespace frt {
 
@@ -55,16 +57,6 @@ struct NodeRec {
 };
 static_assert(sizeof(NodeRec) == 216, "NodeRec layout");
 
-// what k_shadow reads of a path node, one 64-byte line per node (the shadow
-// pass re-reads it from 100 lanes; keeping it apart from the 216-byte NodeRec
-// keeps the pass's HBM traffic at one line per node)
-struct alignas(64) ShadowHead {
-    double over_point[3];
-    uint64_t key;
-    int32_t material;  // -1: the ray missed
-    int32_t pad[5];
-};
-static_assert(sizeof(ShadowHead) == 64, "ShadowHead layout");
 
 struct QueuedRay {
     double o[3];
@@ -76,33 +68,7 @@ struct QueuedRay {
 
 enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ULL;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebULL;
-    x ^= x >> 31;
-    return x;
-}
 
-// area-light cache row for (path node, light, draw): the reference draws
-// rand() % cache_len twice per (hit, light) (light.c:196, renderer.c:915);
-// with a single-row cache both are row 0, as in the reference
-__device__ __forceinline__ int light_row(const frt_light& L, uint64_t seed, uint64_t key, int light, int draw) {
-    if (L.rows <= 1) return 0;
-    uint64_t h = mix64(seed ^ mix64(key * 0x9e3779b97f4a7c15ULL + (uint64_t)(light * 2 + draw + 1)));
-    return (int)(h % (uint64_t)L.rows);
-}
-
-struct Batch {
-    int64_t sample_begin;  // first global sample index of the batch
-    int64_t pixel_begin;   // first pixel (in render order) of the batch
-    int64_t num_samples;
-    int64_t row_begin, row_stride;
-    uint64_t seed;
-    int32_t spp, level;
-    int32_t remaining;     // path_length - level
-};
 
 // ---- stochastic camera sampling (counter-based RNG; the reference draws drand48) ----
 // Uniform double in [0, 1) for draw d of stream (seed, key): 53 bits of a splitmix64 hash.
@@ -411,56 +377,43 @@ __global__ void __launch_bounds__(kTraceBlock) FRT_SHADOW_ATTR k_shadow(DevScene
                                                         const int32_t* __restrict__ j_light,
                                                         const int32_t* __restrict__ j_point, int32_t samples_per_node,
                                                         int32_t* __restrict__ counts, unsigned* err) {
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = tid < n * samples_per_node;
-    int64_t node = 0;
-    int light = 0;
-    bool live = false;
-    Ray r{{0, 0, 0}, {0, 0, 1}};
-    double distance = 0.0;
-    if (valid) {
-        node = tid / samples_per_node;
-        const int j = (int)(tid % samples_per_node);
-        light = j_light[j];
-        const int pt = j_point[j];
-        const ShadowHead* nr = shead + node;
-        if (nr->material >= 0) {
-            live = true;
-            const frt_light& L = S.lights[light];
-            const int row = light_row(L, B.seed, nr->key, light, 0);
-            const double* lp = S.light_points + L.points + 3 * ((int64_t)row * L.num_samples + pt);
-            // is_shadowed (renderer.c:74-93)
-            double v[3] = {lp[0] - nr->over_point[0], lp[1] - nr->over_point[1], lp[2] - nr->over_point[2]};
-            distance = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-            r.o[0] = nr->over_point[0];
-            r.o[1] = nr->over_point[1];
-            r.o[2] = nr->over_point[2];
-            normalize3(v, r.d);
-        }
-    }
+    ShadowLane L;
+    shadow_lane(S, B, shead, n, j_light, j_point, samples_per_node, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, L);
     // every lane of the wave takes part in the (wave-coherent) walk
     unsigned e = 0;
     double unused;
 #ifdef FRT_EXPERIMENT_NOWALK
-    const bool lit = live && distance > 0.5;
+    const bool lit = L.live && L.distance > 0.5;
 #else
-    const bool lit = walk<true, kFeat>(S, r, distance, live, unused, frt_walk_smem, e) == 0 && live;
+    const bool lit = walk<true, kFeat>(S, L.r, L.distance, L.live, unused, frt_walk_smem, e) == 0 && L.live;
 #endif
     if (e) atomicOr(err, e);
-    // segmented wave reduction: lanes with the same (node, light) are contiguous
-    const int lane = threadIdx.x & 63;
-    const int64_t key = valid ? node * S.num_lights + light : -1 - (int64_t)lane;
-    const int64_t prev = __shfl_up(key, 1, 64);
-    const bool head = lane == 0 || prev != key;
-    const unsigned long long heads = __ballot(head);
-    const unsigned long long lits = __ballot(lit);
-    if (valid && head) {
-        const unsigned long long above = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
-        const int next = above ? __ffsll((long long)above) - 1 : 64;
-        const unsigned long long seg = (next >= 64 ? ~0ull : ((1ull << next) - 1)) & ~((1ull << lane) - 1);
-        const int c = __popcll(lits & seg);
-        if (c) atomicAdd(counts + key, c);
+    shadow_count(S, L, lit, counts);
+}
+
+// lanes the scene-specialised shadow kernel (frt_jit.cpp) handed back — rays
+// with non-finite components, which its decisions do not cover — through the
+// generic walk; grid-stride over the queue, whole waves per step, one atomic per lit lane
+template <int kFeat>
+__global__ void __launch_bounds__(kTraceBlock) k_shadow_redo(DevScene S, Batch B, const ShadowHead* __restrict__ shead, int64_t n,
+                                                             const int32_t* __restrict__ j_light,
+                                                             const int32_t* __restrict__ j_point, int32_t samples_per_node,
+                                                             int32_t* __restrict__ counts, unsigned* err,
+                                                             const int64_t* __restrict__ redo,
+                                                             const unsigned* __restrict__ redo_count, unsigned redo_cap) {
+    const unsigned cnt = min(*redo_count, redo_cap);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned e = 0;
+    for (int64_t base = wave * 64; base < (int64_t)cnt; base += nwaves * 64) {
+        const int64_t k = base + (threadIdx.x & 63);
+        ShadowLane L;
+        shadow_lane(S, B, shead, n, j_light, j_point, samples_per_node, k < (int64_t)cnt ? redo[k] : -1, L);
+        double unused;
+        const bool lit = walk<true, kFeat>(S, L.r, L.distance, L.live, unused, frt_walk_smem, e) == 0 && L.live;
+        if (lit) atomicAdd(counts + L.node * S.num_lights + L.light, 1);
     }
+    if (e) atomicOr(err, e);
 }
 
 // lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725)
@@ -982,6 +935,11 @@ struct frt_scene_handle {
     int32_t* j_point = nullptr;
     int32_t samples_per_node = 0;
     size_t lds_bytes = 0;  // dynamic LDS of the traversal kernels
+    // scene-specialised shadow kernel (frt_jit.hip); nullptr: the generic k_shadow runs
+    void* jit_shadow = nullptr;
+    int64_t* redo = nullptr;           // lanes handed back to the generic walk
+    unsigned* redo_count = nullptr;
+    unsigned redo_cap = 0;
     // work buffers (grow on demand)
     struct Level {
         frt::NodeRec* rec = nullptr;
@@ -1085,6 +1043,130 @@ int frt_device_count(void) {
     return n;
 }
 
+// walk visit records (frt_traverse.hpp WalkNode) of the flattened tree
+static void build_walk_nodes(const frt_scene* sc, std::vector<frt::WalkNode>& wn) {
+    auto invert4 = [](const double* m, double* out) -> bool {  // Gauss-Jordan, partial pivoting
+        double a[4][8];
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 8; ++c) a[r][c] = c < 4 ? m[4 * r + c] : (c - 4 == r ? 1.0 : 0.0);
+        for (int c = 0; c < 4; ++c) {
+            int p = c;
+            for (int r = c + 1; r < 4; ++r)
+                if (std::fabs(a[r][c]) > std::fabs(a[p][c])) p = r;
+            if (a[p][c] == 0.0) return false;
+            for (int k = 0; k < 8; ++k) std::swap(a[c][k], a[p][k]);
+            const double inv = 1.0 / a[c][c];
+            for (int k = 0; k < 8; ++k) a[c][k] *= inv;
+            for (int r = 0; r < 4; ++r)
+                if (r != c) {
+                    const double f = a[r][c];
+                    for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
+                }
+        }
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) out[4 * r + c] = a[r][4 + c];
+        return true;
+    };
+    wn.assign((size_t)std::max(1, sc->num_nodes), frt::WalkNode{});
+    for (int i = 0; i < sc->num_nodes; ++i) {
+        const frt_node& nd = sc->nodes[i];
+        frt::WalkNode& w = wn[(size_t)i];
+        std::memset(&w, 0, sizeof(w));
+        w.type = nd.type;
+        w.skip = nd.skip;
+        w.right = nd.right;
+        w.op = nd.type == FRT_CSG ? nd.prim : 0;
+        w.prim = nd.type == FRT_CSG || nd.type == FRT_GROUP ? 0 : nd.prim;
+        w.has_xf = nd.xform >= 0 ? 1 : 0;
+        const int m = nd.material;
+        w.casts = (m >= 0 && m < sc->num_materials && sc->materials[m].casts_shadow) ? 1 : 0;
+        for (int k = 0; k < 6; ++k) {
+            w.bbox[k] = nd.bbox[k];
+            w.bb32[k] = (float)nd.bbox[k];
+        }
+        for (int a = 0; a < 3; ++a)  // rounded up: box32's error bound must not shrink
+            w.bmag[a] = std::nextafter((float)std::max(std::fabs(nd.bbox[a]), std::fabs(nd.bbox[a + 3])), INFINITY);
+        const double* mi = nd.xform >= 0 ? sc->xforms + 16 * (size_t)nd.xform : nullptr;
+        if (mi)
+            for (int k = 0; k < 12; ++k) w.m[k] = mi[k];
+        for (int r = 0; r < 3; ++r) {
+            w.mrow_l1[r] = 0.f;
+            for (int c = 0; c < 3; ++c) {
+                const double v = mi ? mi[4 * r + c] : (r == c ? 1.0 : 0.0);
+                w.mrow[3 * r + c] = (float)v;
+                w.mrow_l1[r] += (float)std::fabs(v);
+            }
+            w.mrow_l1[r] *= 1.0001f;
+        }
+        // prefilter bound in the parent frame (frt_traverse.hpp): cubes, spheres and transformed composites
+        const bool composite = nd.type == FRT_GROUP || nd.type == FRT_CSG;
+        const bool want = nd.type == FRT_CUBE || nd.type == FRT_SPHERE || (composite && mi);
+        double fwd[16];
+        bool ok = want && (!mi || invert4(mi, fwd));
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        if (ok && nd.type == FRT_SPHERE) {
+            for (int a = 0; a < 3; ++a) {
+                const double c = mi ? fwd[4 * a + 3] : 0.0;
+                const double e = mi ? std::sqrt(fwd[4 * a] * fwd[4 * a] + fwd[4 * a + 1] * fwd[4 * a + 1] +
+                                                fwd[4 * a + 2] * fwd[4 * a + 2])
+                                    : 1.0;
+                lo[a] = c - e;
+                hi[a] = c + e;
+            }
+        } else if (ok) {
+            const double bl[3] = {composite ? nd.bbox[0] : -1.0, composite ? nd.bbox[1] : -1.0,
+                                  composite ? nd.bbox[2] : -1.0};
+            const double bh[3] = {composite ? nd.bbox[3] : 1.0, composite ? nd.bbox[4] : 1.0,
+                                  composite ? nd.bbox[5] : 1.0};
+            for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(bl[a]) && std::isfinite(bh[a]);
+            for (int c = 0; ok && c < 8; ++c) {
+                const double p[3] = {(c & 1) ? bh[0] : bl[0], (c & 2) ? bh[1] : bl[1], (c & 4) ? bh[2] : bl[2]};
+                for (int a = 0; a < 3; ++a) {
+                    const double v = mi ? fwd[4 * a] * p[0] + fwd[4 * a + 1] * p[1] + fwd[4 * a + 2] * p[2] +
+                                              fwd[4 * a + 3]
+                                        : p[a];
+                    lo[a] = std::min(lo[a], v);
+                    hi[a] = std::max(hi[a], v);
+                }
+            }
+        }
+        for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(lo[a]) && std::isfinite(hi[a]);
+        if (ok) {
+            for (int a = 0; a < 3; ++a) {
+                const double pad = 1e-7 * ((hi[a] - lo[a]) + std::max(std::fabs(lo[a]), std::fabs(hi[a]))) + 1e-12;
+                w.pbox[a] = lo[a] - pad;
+                w.pbox[a + 3] = hi[a] + pad;
+            }
+            w.pre = 1 | (nd.type == FRT_SPHERE ? 0 : 2);
+        } else {
+            w.pre = 0;
+        }
+    }
+}
+
+// TEST INFRASTRUCTURE / diagnostics (include/frt_device.h): generate and compile the scene-specialised
+// shadow kernel of a flattened scene without a device. Returns 0 compiled, 1 not eligible, -1 compile error;
+// `log` receives the reason / compiler log, `src` (if non-null) the generated source.
+int frt_jit_check(const frt_scene* sc, char* log, size_t log_cap, char* src, size_t src_cap) {
+    std::vector<frt::WalkNode> wn;
+    build_walk_nodes(sc, wn);
+    std::string why, clog;
+    const std::string code = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, why);
+    auto put = [](char* dst, size_t cap, const std::string& v) {
+        if (dst && cap) {
+            std::snprintf(dst, cap, "%s", v.c_str());
+        }
+    };
+    put(src, src_cap, code);
+    if (code.empty()) {
+        put(log, log_cap, why);
+        return 1;
+    }
+    const int rc = frt_jit_compile_only(code, "gfx950", clog);
+    put(log, log_cap, clog);
+    return rc == 0 ? 0 : -1;
+}
+
 const char* frt_last_error(void) { return g_last_error.c_str(); }
 
 int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
@@ -1123,100 +1205,32 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         return -1;
     }
     {
-        // walk visit records (frt_traverse.hpp WalkNode)
-        auto invert4 = [](const double* m, double* out) -> bool {  // Gauss-Jordan, partial pivoting
-            double a[4][8];
-            for (int r = 0; r < 4; ++r)
-                for (int c = 0; c < 8; ++c) a[r][c] = c < 4 ? m[4 * r + c] : (c - 4 == r ? 1.0 : 0.0);
-            for (int c = 0; c < 4; ++c) {
-                int p = c;
-                for (int r = c + 1; r < 4; ++r)
-                    if (std::fabs(a[r][c]) > std::fabs(a[p][c])) p = r;
-                if (a[p][c] == 0.0) return false;
-                for (int k = 0; k < 8; ++k) std::swap(a[c][k], a[p][k]);
-                const double inv = 1.0 / a[c][c];
-                for (int k = 0; k < 8; ++k) a[c][k] *= inv;
-                for (int r = 0; r < 4; ++r)
-                    if (r != c) {
-                        const double f = a[r][c];
-                        for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
-                    }
-            }
-            for (int r = 0; r < 4; ++r)
-                for (int c = 0; c < 4; ++c) out[4 * r + c] = a[r][4 + c];
-            return true;
-        };
-        std::vector<frt::WalkNode> wn((size_t)std::max(1, sc->num_nodes));
-        for (int i = 0; i < sc->num_nodes; ++i) {
-            const frt_node& nd = sc->nodes[i];
-            frt::WalkNode& w = wn[(size_t)i];
-            std::memset(&w, 0, sizeof(w));
-            w.type = nd.type;
-            w.skip = nd.skip;
-            w.right = nd.right;
-            w.op = nd.type == FRT_CSG ? nd.prim : 0;
-            w.prim = nd.type == FRT_CSG || nd.type == FRT_GROUP ? 0 : nd.prim;
-            w.has_xf = nd.xform >= 0 ? 1 : 0;
-            const int m = nd.material;
-            w.casts = (m >= 0 && m < sc->num_materials && sc->materials[m].casts_shadow) ? 1 : 0;
-            for (int k = 0; k < 6; ++k) w.bbox[k] = nd.bbox[k];
-            const double* mi = nd.xform >= 0 ? sc->xforms + 16 * (size_t)nd.xform : nullptr;
-            if (mi)
-                for (int k = 0; k < 12; ++k) w.m[k] = mi[k];
-            for (int r = 0; r < 3; ++r) {
-                w.mrow_l1[r] = 0.f;
-                for (int c = 0; c < 3; ++c) {
-                    const double v = mi ? mi[4 * r + c] : (r == c ? 1.0 : 0.0);
-                    w.mrow[3 * r + c] = (float)v;
-                    w.mrow_l1[r] += (float)std::fabs(v);
-                }
-                w.mrow_l1[r] *= 1.0001f;
-            }
-            // prefilter bound in the parent frame (frt_traverse.hpp): cubes, spheres and transformed composites
-            const bool composite = nd.type == FRT_GROUP || nd.type == FRT_CSG;
-            const bool want = nd.type == FRT_CUBE || nd.type == FRT_SPHERE || (composite && mi);
-            double fwd[16];
-            bool ok = want && (!mi || invert4(mi, fwd));
-            double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-            if (ok && nd.type == FRT_SPHERE) {
-                for (int a = 0; a < 3; ++a) {
-                    const double c = mi ? fwd[4 * a + 3] : 0.0;
-                    const double e = mi ? std::sqrt(fwd[4 * a] * fwd[4 * a] + fwd[4 * a + 1] * fwd[4 * a + 1] +
-                                                    fwd[4 * a + 2] * fwd[4 * a + 2])
-                                        : 1.0;
-                    lo[a] = c - e;
-                    hi[a] = c + e;
-                }
-            } else if (ok) {
-                const double bl[3] = {composite ? nd.bbox[0] : -1.0, composite ? nd.bbox[1] : -1.0,
-                                      composite ? nd.bbox[2] : -1.0};
-                const double bh[3] = {composite ? nd.bbox[3] : 1.0, composite ? nd.bbox[4] : 1.0,
-                                      composite ? nd.bbox[5] : 1.0};
-                for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(bl[a]) && std::isfinite(bh[a]);
-                for (int c = 0; ok && c < 8; ++c) {
-                    const double p[3] = {(c & 1) ? bh[0] : bl[0], (c & 2) ? bh[1] : bl[1], (c & 4) ? bh[2] : bl[2]};
-                    for (int a = 0; a < 3; ++a) {
-                        const double v = mi ? fwd[4 * a] * p[0] + fwd[4 * a + 1] * p[1] + fwd[4 * a + 2] * p[2] +
-                                                  fwd[4 * a + 3]
-                                            : p[a];
-                        lo[a] = std::min(lo[a], v);
-                        hi[a] = std::max(hi[a], v);
-                    }
-                }
-            }
-            for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(lo[a]) && std::isfinite(hi[a]);
-            if (ok) {
-                for (int a = 0; a < 3; ++a) {
-                    const double pad = 1e-7 * ((hi[a] - lo[a]) + std::max(std::fabs(lo[a]), std::fabs(hi[a]))) + 1e-12;
-                    w.pbox[a] = lo[a] - pad;
-                    w.pbox[a + 3] = hi[a] + pad;
-                }
-                w.pre = 1 | (nd.type == FRT_SPHERE ? 0 : 2);
-            } else {
-                w.pre = 0;
-            }
-        }
+        std::vector<frt::WalkNode> wn;
+        build_walk_nodes(sc, wn);
         S.wn = upload(h, wn.data(), wn.size(), rc);
+        const char* jit_env = std::getenv("FRT_JIT");
+        if (rc == 0 && sc->config.include_direct && !(jit_env && std::strcmp(jit_env, "0") == 0)) {
+            std::string why, log;
+            const std::string src = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, why);
+            if (!src.empty() && frt_jit_compile(src, h->device, &h->jit_shadow, log) != 0) {
+                why = "hiprtc: " + log.substr(0, 2000);
+                h->jit_shadow = nullptr;
+            }
+            if (h->jit_shadow) {
+                h->redo_cap = 1u << 20;
+                void* p = nullptr;
+                if (hipMalloc(&p, h->redo_cap * sizeof(int64_t) + 64) != hipSuccess) {
+                    frt_scene_release(h);
+                    return fail("frt_scene_upload: redo queue allocation failed");
+                }
+                h->owned.push_back(p);
+                h->redo = (int64_t*)p;
+                h->redo_count = (unsigned*)(h->redo + h->redo_cap);
+            } else if (std::getenv("FRT_JIT_VERBOSE")) {
+                std::fprintf(stderr, "frt: generic shadow walk (%s)\n", why.c_str());
+            }
+            if (std::getenv("FRT_JIT_DUMP") && !src.empty()) std::fprintf(stderr, "%s\n", src.c_str());
+        }
     }
     {
         // per-lane walk capacities (see frt_traverse.hpp): exact bounds from the tree
@@ -1282,9 +1296,9 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             return -1;
         }
     }
-#ifdef FRT_WALK_STATS
-    if (hipMalloc((void**)&h->S.dbg, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(h->S.dbg, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+#if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)
+    if (hipMalloc((void**)&h->S.dbg, frt::kDbgSlots * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(h->S.dbg, 0, frt::kDbgSlots * sizeof(unsigned long long)) != hipSuccess) {
         frt_scene_release(h);
         return fail("frt_scene_upload: debug counters");
     }
@@ -1437,7 +1451,30 @@ static void launch_shadow_f(frt_scene_handle* h, const frt::Batch& B, const frt:
                        h->stream, h->S, B, rec, n, h->j_light, h->j_point, h->samples_per_node, counts, h->err);
 }
 
+template <int F>
+static void launch_shadow_redo_f(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n,
+                                 int32_t* counts) {
+    hipLaunchKernelGGL(frt::k_shadow_redo<F>, dim3(64), dim3(frt::kTraceBlock), h->lds_bytes, h->stream, h->S, B, rec, n,
+                       h->j_light, h->j_point, h->samples_per_node, counts, h->err, h->redo, h->redo_count, h->redo_cap);
+}
+
 static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts) {
+    if (h->jit_shadow) {
+        // scene-specialised kernel, then the generic walk over the lanes it handed back (usually none)
+        int64_t work = n * h->samples_per_node;
+        hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
+        void* args[] = {&h->S, (void*)&B, (void*)&rec, &n, &h->j_light, &h->j_point, &h->samples_per_node,
+                        &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err};
+        hip_ignore(hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(work, frt::kTraceBlock), 1, 1,
+                                         frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr));
+        switch (h->S.features & 3) {
+        case 0: launch_shadow_redo_f<0>(h, B, rec, n, counts); break;
+        case 1: launch_shadow_redo_f<1>(h, B, rec, n, counts); break;
+        case 2: launch_shadow_redo_f<2>(h, B, rec, n, counts); break;
+        default: launch_shadow_redo_f<3>(h, B, rec, n, counts); break;
+        }
+        return;
+    }
     switch (h->S.features & 3) {
     case 0: launch_shadow_f<0>(h, B, rec, n, counts); break;
     case 1: launch_shadow_f<1>(h, B, rec, n, counts); break;
@@ -1671,10 +1708,10 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
 
 extern "C" {
 
-#ifdef FRT_WALK_STATS
+#if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)
 // debug builds: dump the walk counters accumulated so far to stderr
 static void dump_walk_stats(frt_scene_handle* h) {
-    unsigned long long c[16];
+    unsigned long long c[frt::kDbgSlots];
     if (hipMemcpy(c, h->S.dbg, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) return;
     const char* names[8] = {"composite_visits", "leaf_visits", "active_lane_visits", "jumps", "walks", "live_lanes",
                             "prefilter_rejects", "lanes_tested"};
@@ -1683,6 +1720,19 @@ static void dump_walk_stats(frt_scene_handle* h) {
         for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %s=%llu", names[j], c[8 * k + j]);
         std::fprintf(stderr, "\n");
     }
+    // per node: wave visits / active lanes (shadow, then closest hit)
+    for (int k = 0; k < 2; ++k) {
+        std::fprintf(stderr, "node visits (%s):", k == 0 ? "shadow" : "closest");
+        for (int i = 0; i < std::min(h->S.num_nodes, frt::kDbgNodes); ++i) {
+            const unsigned long long* v = c + 16 + (k * frt::kDbgNodes + i) * 2;
+            if (v[0]) std::fprintf(stderr, " %d:%llu/%llu", i, v[0], v[1]);
+        }
+        std::fprintf(stderr, "\n");
+    }
+    std::fprintf(stderr, "walk prof (shadow, cycles):");
+    const char* pn[8] = {"setup", "close", "xf_pop", "composite", "leaf_xf", "leaf_test", "leaf_post", "loop"};
+    for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s=%llu", pn[k], c[frt::kDbgProf + k]);
+    std::fprintf(stderr, "\n");
 }
 #endif
 
@@ -1835,9 +1885,10 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         st->shadow_kernel_bytes =
             h->S.cfg.include_direct && h->samples_per_node > 0 ? (double)host_counters[17] * (64.0 + 4.0 * h->S.num_lights) : 0.0;
         st->errors = err;
+        st->shadow_jit = h->jit_shadow != nullptr ? 1 : 0;
         collect_timings(h, st);
     }
-#ifdef FRT_WALK_STATS
+#if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)
     dump_walk_stats(h);
 #endif
     if (err) {

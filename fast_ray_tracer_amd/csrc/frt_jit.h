@@ -1,0 +1,21 @@
+// frt-mi355x scene-specialised shadow kernel (frt_jit.hip): host interface used by the engine.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+
+namespace frt {
+struct WalkNode;
+}
+
+// HIP source of the shadow kernel for this tree ("" and `why` set when the scene
+// is not eligible: too many nodes, or a CSG unit with a leaf whose list is unsorted)
+std::string frt_jit_shadow_source(const frt::WalkNode* wn, int num_nodes, const int32_t* roots, int num_roots,
+                                  std::string& why);
+
+// compile with hiprtc for `device` (cached per device and source); 0 on success, *fn = hipFunction_t
+int frt_jit_compile(const std::string& src, int device, void** fn, std::string& log);
+
+// compile only (no device needed): 0 on success
+int frt_jit_compile_only(const std::string& src, const std::string& arch, std::string& log);

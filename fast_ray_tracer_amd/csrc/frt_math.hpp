@@ -5,8 +5,10 @@
 // ISO-C build.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (frt_jit.cpp) provides the HIP runtime and fixed-width types itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "frt_device.h"
 
@@ -174,6 +176,61 @@ __device__ __forceinline__ bool box_decide(const double* bb, const Ray& r, const
     if (tmin > tmax + margin) return false;
     double a, b;
     return box_range(bb, r, a, b);
+}
+
+// ---- binary32 box decisions with a rigorous error bound ----
+// The reference decides a box hit as tmin <= tmax over binary64 slab quotients
+// (lo - o) / d (bounding_box.c:124-175). Here the quotients come from binary32
+// operands: o' = f32(o), lo' = f32(lo), r = v_rcp_f32(f32(d)) (1 ulp), t' = (lo' - o') * r.
+// Per axis |t' - t| <= (|lo' - lo| + |o' - o| + u|lo - o|)/|d| + |t|(|r d - 1|) + u|t'|
+//                  <= (2.01 + 3.01 + 1.01) u (|lo| + |o|) / |d| + O(u^2)     (|t| <= (|lo|+|o|)/|d|)
+// with u = 2^-24, so with mag = max(|lo|, |hi|) rounded up, every slab value and
+// hence tmin / tmax (max / min of them) are within E = 7u max_a (mag_a + |o'_a|) |r_a|
+// of the reference's. tmax' - tmin' > 2.01 E proves a hit, < -2.01 E a miss; in
+// between the binary64 test decides. The |d| < EPSILON branch (infinite slabs) is
+// never taken here: a frame whose f32 direction has a component below kEps32 is
+// decided in binary64 throughout (Frame32::exact).
+constexpr float kEps32 = 1.00001e-5f;  // |f32(d)| >= kEps32  =>  |d| >= EPSILON
+constexpr float kBox32Err = 7.0f * 0x1p-24f;
+
+struct Frame32 {
+    float o[3];  // f32(origin)
+    float r[3];  // v_rcp_f32(f32(direction))
+    bool exact;  // a direction component may be below EPSILON: binary64 decisions only
+};
+
+__device__ __forceinline__ void frame32(const Ray& ray, Frame32& f) {
+    bool ex = false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        f.o[a] = (float)ray.o[a];
+        const float d = (float)ray.d[a];
+        f.r[a] = __builtin_amdgcn_rcpf(d);
+        ex = ex || !(fabsf(d) >= kEps32);
+    }
+    f.exact = ex;
+}
+
+// 1: hit, 0: miss, -1: undecided (take the binary64 test). tmin / tmax: the f32
+// estimates, err: their error bound E.
+__device__ __forceinline__ int box32(const float* bb, const float* mag, const Frame32& f, float& tmin, float& tmax,
+                                     float& err) {
+    float lo3[3], hi3[3], e = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float t0 = (bb[a] - f.o[a]) * f.r[a];
+        const float t1 = (bb[a + 3] - f.o[a]) * f.r[a];
+        lo3[a] = fminf(t0, t1);
+        hi3[a] = fmaxf(t0, t1);
+        e = fmaxf(e, (mag[a] + fabsf(f.o[a])) * fabsf(f.r[a]));
+    }
+    tmin = fmaxf(fmaxf(lo3[0], lo3[1]), lo3[2]);
+    tmax = fminf(fminf(hi3[0], hi3[1]), hi3[2]);
+    err = kBox32Err * e + 1e-30f;
+    const float diff = tmax - tmin;
+    if (diff > 2.01f * err) return 1;
+    if (-diff > 2.01f * err) return 0;
+    return -1;
 }
 
 // Conservative line-vs-box test for the prefilter: false only when the exact

@@ -46,6 +46,9 @@ struct alignas(16) WalkNode {
     double pbox[6];                    // prefilter: inflated bound of the node in its parent's frame
     float mrow[9];                     // rows of m's 3x3 part (identity without transform), as float
     float mrow_l1[3];                  // their L1 norms
+    float bb32[6];                     // composites: f32(bbox) (box32)
+    float bmag[3];                     // composites: max(|lo_a|, |hi_a|) rounded up (box32's error bound)
+    int32_t pad32;
 };
 
 // per-frame cache of the current ray: reciprocal direction (two Newton steps),
@@ -106,6 +109,41 @@ struct DevScene {
 };
 
 enum FeatureBits : int { kFeatCsg = 1, kFeatTorus = 2 };
+
+// FRT_WALK_STATS builds: 16 global counters + per node (first kDbgNodes) {wave visits, active lanes} x 2 walks
+constexpr int kDbgNodes = 64;
+constexpr int kDbgSlots = 16 + 4 * kDbgNodes + 16;
+constexpr int kDbgProf = 16 + 4 * kDbgNodes;  // FRT_WALK_PROF builds: s_memtime cycles per walk region (shadow)
+
+#ifdef FRT_WALK_PROF
+__device__ __forceinline__ unsigned long long prof_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define FRT_PROF_DECL unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_last = prof_stamp();
+#define FRT_PROF(k)                              \
+    do {                                         \
+        const unsigned long long now_ = prof_stamp(); \
+        prof_acc[k] += now_ - prof_last;         \
+        prof_last = now_;                        \
+    } while (0)
+#define FRT_PROF_FLUSH                                                                  \
+    do {                                                                                \
+        if (kShadow && (threadIdx.x & 63) == 0)                                         \
+            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(S.dbg + kDbgProf + k_, prof_acc[k_]); \
+    } while (0)
+#else
+#define FRT_PROF_DECL
+#define FRT_PROF(k) \
+    do {            \
+    } while (0)
+#define FRT_PROF_FLUSH \
+    do {               \
+    } while (0)
+#endif
 
 constexpr int kTraceBlock = 128;  // lanes per block of the traversal kernels
 
@@ -293,6 +331,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
     ContainerTop2 ct;
     ct.init();
     bool best_present = false;
+    FRT_PROF_DECL
 #ifdef FRT_WALK_STATS
     {
         const unsigned long long lv = __ballot(live);
@@ -322,7 +361,9 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
         frame_cache(cur, fc);
 #endif
         int i = root;
+        FRT_PROF(0);
         while (true) {
+            FRT_PROF(7);
             // ---- close the composites the walk has left ----
             if constexpr (kCsg) {
                 while (cp > 0) {
@@ -398,6 +439,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                     n = 0;
                 }
             }
+            FRT_PROF(1);
             // ---- pop transform frames, rebuild the ray from the world ray ----
             if (i >= xf_end) {
                 do {
@@ -410,6 +452,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                 frame_cache(cur, fc);
 #endif
             }
+            FRT_PROF(2);
             if (i >= end) break;
             const bool active = i >= resume;
             if (__ballot(active) == 0) {
@@ -432,6 +475,11 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                 if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
                     atomicAdd(S.dbg + (kShadow ? 0 : 8) + ((type == FRT_GROUP || type == FRT_CSG) ? 0 : 1), 1ull);
                     atomicAdd(S.dbg + (kShadow ? 0 : 8) + 2, (unsigned long long)__popcll(av));
+                    if (i < kDbgNodes) {
+                        unsigned long long* pn = S.dbg + 16 + ((kShadow ? 0 : kDbgNodes) + i) * 2;
+                        atomicAdd(pn, 1ull);
+                        atomicAdd(pn + 1, (unsigned long long)__popcll(av));
+                    }
                 }
             }
 #endif
@@ -467,8 +515,17 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                 bool enter = false;
                 if (may) {
                     const Ray lr = nd.has_xf ? xf_ray_walk(nd.m, cur) : cur;
+                    Frame32 lf;
+                    frame32(lr, lf);
+                    // binary32 decision with an error bound (box32), binary64 where it cannot decide
+                    float tmin32 = -1.0f, tmax32 = 1.0f, err32 = 0.0f;
+                    const int dec = (lf.exact || (S.walk_flags & 2)) ? -1 : box32(nd.bb32, nd.bmag, lf, tmin32, tmax32, err32);
                     double tmin = -1.0, tmax = 1.0;
-                    if (origin_inside(nd.bbox, lr)) {
+                    if (dec >= 0) {
+                        enter = dec != 0;
+                        tmin = (double)tmin32 - (double)err32;  // bounds on the reference's tmin / tmax
+                        tmax = (double)tmax32 + (double)err32;
+                    } else if (origin_inside(nd.bbox, lr)) {
                         enter = true;
                     } else if (S.walk_flags & 2) {
                         enter = box_range(nd.bbox, lr, tmin, tmax);
@@ -484,6 +541,7 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                     }
                 }
                 if (active && !enter) resume = nd.skip;
+                FRT_PROF(3);
                 if (__ballot(enter) == 0) {
                     i = nd.skip;
                     continue;
@@ -528,8 +586,10 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
             if (may) {
                 const Ray lr = nd.has_xf ? xf_ray_walk(nd.m, cur) : cur;
                 LeafHits H;
+                FRT_PROF(4);
                 if (kShadow && cp == 0 && type == FRT_CUBE && !(S.walk_flags & 4)) cube_hits_for_decisions(lr, distance, H);
                 else leaf_hits<kTorus>(type, S.prim + nd.prim, lr, H);
+                FRT_PROF(5);
                 if (kCsg && cp > 0) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -589,11 +649,13 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
                     }
                 }
             }
+            FRT_PROF(6);
             ++i;
         }
         if (kShadow && live && resume != kDone && any_entry) live = false;  // first world shape with entries ends it
         if (resume == kDone) live = false;
     }
+    FRT_PROF_FLUSH;
     if (!kShadow && n12 != nullptr) {
         n12[0] = 1.0;
         n12[1] = 1.0;

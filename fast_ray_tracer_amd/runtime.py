@@ -34,7 +34,8 @@ class FrameStats(ctypes.Structure):
                 ("hits", ctypes.c_uint64), ("errors", ctypes.c_uint64), ("render_ms", ctypes.c_double),
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_uint64 * 8),
                 ("shadow_kernel_bytes", ctypes.c_double), ("gather_rays", ctypes.c_uint64),
-                ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double)]
+                ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double),
+                ("shadow_jit", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
@@ -44,7 +45,7 @@ class FrameStats(ctypes.Structure):
             "hits": int(self.hits), "errors": int(self.errors), "render_ms": float(self.render_ms),
             "shadow_kernel_bytes": float(self.shadow_kernel_bytes),
             "gather_rays": int(self.gather_rays), "photons": [int(self.photons[0]), int(self.photons[1])],
-            "photon_ms": float(self.photon_ms),
+            "photon_ms": float(self.photon_ms), "shadow_jit": int(self.shadow_jit),
             "kernel_ms": {names[i]: float(self.kernel_ms[i]) for i in range(8) if self.kernel_launches[i]},
             "kernel_launches": {names[i]: int(self.kernel_launches[i]) for i in range(8) if self.kernel_launches[i]},
         }
@@ -184,6 +185,31 @@ class GpuRenderer:
         if rc != 0:
             raise RuntimeError("frt render failed: " + self.lib.frt_last_error().decode())
         return st if stats else None
+
+
+def jit_check(scene: Scene) -> tuple[int, str, str]:
+    """Generate and compile (hiprtc, no device needed) the scene-specialised shadow
+    kernel frt_scene_upload would use for this scene: (rc, log, source) with rc 0
+    compiled, 1 not eligible (generic walk), -1 compile error (include/frt_device.h)."""
+    lib = host_lib()
+    vp = ctypes.c_void_p
+    lib.frt_flatten_scene.restype = ctypes.c_int
+    lib.frt_flatten_scene.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool, vp, ctypes.c_char_p,
+                                      ctypes.c_size_t]
+    lib.frt_flat_scene_free.argtypes = [vp]
+    lib.frt_jit_check.restype = ctypes.c_int
+    lib.frt_jit_check.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    fs = ctypes.create_string_buffer(4096)  # frt_scene (a few hundred bytes)
+    err = ctypes.create_string_buffer(512)
+    if lib.frt_flatten_scene(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter, fs, err, 512):
+        raise RuntimeError("frt: flatten failed: " + err.value.decode())
+    log = ctypes.create_string_buffer(1 << 16)
+    src = ctypes.create_string_buffer(1 << 22)
+    try:
+        rc = lib.frt_jit_check(fs, log, len(log), src, len(src))
+    finally:
+        lib.frt_flat_scene_free(fs)
+    return rc, log.value.decode(errors="replace"), src.value.decode(errors="replace")
 
 
 def encode_ppm(rgba: np.ndarray, use_scaling: bool = True) -> bytes:

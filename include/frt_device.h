@@ -24,8 +24,10 @@
 #ifndef FRT_DEVICE_H
 #define FRT_DEVICE_H
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -212,6 +214,8 @@ typedef struct frt_frame_stats {
     uint64_t gather_rays;         /* final-gather rays traced (global illumination) */
     uint64_t photons[2];          /* photons in the caustic / global map used by this frame */
     double photon_ms;             /* photon tracing + map build of this frame (0 when the maps were reused) */
+    int32_t shadow_jit;           /* 1: the scene-specialised shadow kernel ran (frt_jit.hip), 0: the generic walk */
+    int32_t pad;
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */
@@ -232,6 +236,12 @@ int frt_render_rows_device(frt_scene_handle *h, const frt_frame_params *params, 
                            frt_frame_stats *stats);
 
 void frt_scene_release(frt_scene_handle *h);
+
+/* Diagnostics (no device needed): generate the scene-specialised shadow kernel of a flattened
+ * scene and compile it for gfx950 with hiprtc, as frt_scene_upload does. Returns 0 compiled,
+ * 1 scene not eligible (the generic walk runs), -1 compile error. `log` receives the reason or
+ * the compiler log, `src` (may be NULL) the generated HIP source. */
+int frt_jit_check(const frt_scene *scene, char *log, size_t log_cap, char *src, size_t src_cap);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,7 @@
 set -o pipefail
 TAG=${1:-chk}; shift
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 tail -4 gpurun_out/pytest_$TAG.log
 [ $rc -ne 0 ] && exit $rc
