@@ -36,6 +36,7 @@
 #include "frt_jit.h"
 #include "frt_shade.hpp"
 #include "frt_shadow.hpp"
+#include "frt_cols.hpp"
 
 namespace frt {
 
@@ -66,7 +67,8 @@ struct QueuedRay {
     int32_t slot;
 };
 
-enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8 };
+// k*Spawned: the child ray was queued (its k_combine writes the parent's slot; otherwise the slot reads as 0)
+enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8, kReflSpawned = 16, kRefrSpawned = 32 };
 
 
 
@@ -208,7 +210,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
     // every lane of the wave takes part in the (wave-coherent) walk; queued rays with
     // parent < -1 are placeholders (final-gather slots of nodes without a gather)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = i < n && (q == nullptr || q[i].parent >= -1);
+    const bool live = i < n && (q == nullptr || q[queue_slot(B, i)].parent >= -1);
     Ray r{{0, 0, 0}, {0, 0, 1}};
     unsigned e = 0;
     if (live) {
@@ -216,7 +218,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
             uint64_t key;
             camera_ray(S, B, i, r, key, e);
         } else {
-            const QueuedRay& qr = q[i];
+            const QueuedRay& qr = q[queue_slot(B, i)];
             for (int k = 0; k < 3; ++k) {
                 r.o[k] = qr.o[k];
                 r.d[k] = qr.d[k];
@@ -231,13 +233,27 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
 }
 
 // prepare_computations + spawn of the reflection / refraction rays (renderer.c:369-605)
+template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
-                                                    const HitRec* __restrict__ hits, NodeRec* __restrict__ rec,
+                                                    const HitRec* __restrict__ hits, Cols<NodeRec> rec,
                                                     ShadowHead* __restrict__ heads,
-                                                    QueuedRay* __restrict__ next_q, int64_t next_cap,
-                                                    unsigned long long* next_count, unsigned long long* counters,
-                                                    unsigned* err) {
+                                                    QueuedRay* __restrict__ next_q,
+                                                    unsigned long long* counters, unsigned* err) {
+    // this block's counter line: next-level queue segment count (word level + 1), pruned (16), hits (17)
+    unsigned long long* line = counters + kCounterLine * (blockIdx.x % kQueueSegs);
+    const int64_t seg_base = (int64_t)(blockIdx.x % kQueueSegs) * B.next_segcap;
     const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#ifdef FRT_WALK_PROF
+    unsigned long long pt0 = prof_stamp();
+    auto pstamp = [&](int k) {
+        const unsigned long long t1 = prof_stamp();
+        if ((threadIdx.x & 63) == 0) atomicAdd(S.dbg + kDbgProf + 8 + k, t1 - pt0);
+        pt0 = t1;
+    };
+#define PSTAMP(k) pstamp(k)
+#else
+#define PSTAMP(k)
+#endif
     if (node >= n) return;
     Ray r;
     uint64_t key;
@@ -246,7 +262,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
         unsigned ce = 0;
         camera_ray(S, B, node, r, key, ce);
     } else {
-        const QueuedRay& qr = q[node];
+        const QueuedRay& qr = q[queue_slot(B, node)];
         for (int k = 0; k < 3; ++k) {
             r.o[k] = qr.o[k];
             r.d[k] = qr.d[k];
@@ -255,20 +271,25 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
         parent = qr.parent;
         slot = qr.slot;
     }
+    PSTAMP(0);
     const HitRec hr = hits[node];
+    PSTAMP(1);
     if (hr.node < 0) {
-        rec[node].material = -1;
-        rec[node].parent = parent;
-        rec[node].slot = slot;
+        NodeRec miss{};
+        miss.material = -1;
+        miss.parent = parent;
+        miss.slot = slot;
+        rec.store(node, miss);
         heads[node].material = -1;
         return;
     }
     Hit h{hr.t, -1, -1, hr.node};
     Comps c;
-    prepare(S, r, h, c);
+    prepare<kPat>(S, r, h, c);
     c.n1 = hr.n1;
     c.n2 = hr.n2;
-    atomicAdd(counters + 1, 1ull);  // shaded path nodes
+    PSTAMP(2);
+    wave_count(line + 17, true);  // shaded path nodes
     const frt_material& M = S.materials[c.material];
     NodeRec nr;
     for (int k = 0; k < 3; ++k) {
@@ -318,9 +339,18 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
         const uint64_t code = key & 0xFFFull;
         const uint64_t base = key & ~0xFFFull;
         // spawn only children whose weight can be non-zero (zero-weight subtrees add exactly 0)
-        if (reflect_applies && (c.refl[0] != 0.0 || c.refl[1] != 0.0 || c.refl[2] != 0.0)) {
-            unsigned long long at = atomicAdd(next_count, 1ull);
-            if ((int64_t)at < next_cap) {
+        const bool want_refl = reflect_applies && (c.refl[0] != 0.0 || c.refl[1] != 0.0 || c.refl[2] != 0.0);
+        const bool tf_zero = M.Tf[0] == 0.0 && M.Tf[1] == 0.0 && M.Tf[2] == 0.0;
+        const bool want_refr = refract_applies && !tf_zero;
+        if (want_refl) flags |= kReflSpawned;
+        if (want_refr) flags |= kRefrSpawned;
+        // slots in this block's segment of the next level's queue
+        const unsigned long long at_refl = wave_append(line + B.level + 1, want_refl);
+        const unsigned long long at_refr = wave_append(line + B.level + 1, want_refr);
+        wave_count(line + 16, reflect_applies && !want_refl);  // pruned zero-weight rays
+        wave_count(line + 16, refract_applies && !want_refr);
+        if (want_refl) {
+            if ((int64_t)at_refl < B.next_segcap) {
                 QueuedRay qo;
                 for (int k = 0; k < 3; ++k) {
                     qo.o[k] = c.over_point[k];
@@ -329,17 +359,13 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
                 qo.key = base | ((code * 2) & 0xFFFull);
                 qo.parent = (int32_t)node;
                 qo.slot = 0;
-                next_q[at] = qo;
+                next_q[seg_base + (int64_t)at_refl] = qo;
             } else {
                 atomicOr(err, kErrQueueOverflow);
             }
-        } else if (reflect_applies) {
-            atomicAdd(counters, 1ull);
         }
-        const bool tf_zero = M.Tf[0] == 0.0 && M.Tf[1] == 0.0 && M.Tf[2] == 0.0;
-        if (refract_applies && !tf_zero) {
-            unsigned long long at = atomicAdd(next_count, 1ull);
-            if ((int64_t)at < next_cap) {
+        if (want_refr) {
+            if ((int64_t)at_refr < B.next_segcap) {
                 QueuedRay qo;
                 for (int k = 0; k < 3; ++k) {
                     qo.o[k] = c.under_point[k];
@@ -348,22 +374,22 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
                 qo.key = base | ((code * 2 + 1) & 0xFFFull);
                 qo.parent = (int32_t)node;
                 qo.slot = 1;
-                next_q[at] = qo;
+                next_q[seg_base + (int64_t)at_refr] = qo;
             } else {
                 atomicOr(err, kErrQueueOverflow);
             }
-        } else if (refract_applies) {
-            atomicAdd(counters, 1ull);
         }
     }
     nr.flags = flags;
-    rec[node] = nr;
+    PSTAMP(3);
+    rec.store(node, nr);
     ShadowHead hd;
     for (int k = 0; k < 3; ++k) hd.over_point[k] = c.over_point[k];
     hd.key = key;
     hd.material = c.material;
     for (int k = 0; k < 5; ++k) hd.pad[k] = 0;
     heads[node] = hd;
+    PSTAMP(4);
 }
 
 // one lane per (node, light sample j); lanes of a node are consecutive
@@ -417,11 +443,11 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow_redo(DevScene S, Batch B
 }
 
 // lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725)
-__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, const NodeRec* __restrict__ rec, int64_t n,
-                                                  const int32_t* __restrict__ counts, double* __restrict__ surface) {
+__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<NodeRec> rec, int64_t n,
+                                                  const int32_t* __restrict__ counts, Cols<Tri9> surface) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec& nr = rec[i];
+    const NodeRec nr = rec.load(i);
     if (nr.material < 0) return;
     double sA[3] = {0, 0, 0}, sD[3] = {0, 0, 0}, sS[3] = {0, 0, 0};
     if (S.cfg.include_direct) {
@@ -489,34 +515,35 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, const Nod
             }
         }
     }
-    double* out = surface + 12 * i;
+    double out[12];
     for (int k = 0; k < 3; ++k) {
         out[k] = sA[k];
         out[4 + k] = sD[k];
         out[8 + k] = sS[k];
     }
-    out[3] = out[7] = out[11] = 0.0;
+    tri_store(surface, i, out);
 }
 
 // bottom-up combine of one level (shade_hit's specular block, renderer.c:773-822)
-__global__ void __launch_bounds__(kBlock) k_combine(const NodeRec* __restrict__ rec, int64_t n,
-                                                    const double* __restrict__ surface,
-                                                    const double* __restrict__ child,
-                                                    double* __restrict__ parent_child, double* __restrict__ sample_out,
+// (level 0: samples land in sample_out at (sub-sample, pixel) order, coalesced for k_resolve)
+__global__ void __launch_bounds__(kBlock) k_combine(Cols<NodeRec> rec, int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
+                                                    Cols<Tri9> parent_child, Cols<Tri9> sample_out, int32_t spp,
                                                     const frt_material* __restrict__ mats, int32_t include_specular) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec& nr = rec[i];
+    const NodeRec nr = rec.load(i);
     double col[12];
     if (nr.material < 0) {
         for (int k = 0; k < 12; ++k) col[k] = 0.0;
     } else {
-        const double* s = surface + 12 * i;
-        for (int k = 0; k < 12; ++k) col[k] = s[k];
+        tri_load(surface, i, col);
         if (include_specular) {
             const frt_material& M = mats[nr.material];
-            const double* R = child + 24 * i;
-            const double* T = R + 12;
+            // reflected / refracted_color from the children's slots; a child that was not traced
+            // (zero weight, or nothing to spawn) contributes an exact 0
+            double R[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, T[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            if (nr.flags & kReflSpawned) tri_load(child, 2 * i, R);
+            if (nr.flags & kRefrSpawned) tri_load(child, 2 * i + 1, T);
             double rl[12], rr[12];
             for (int t = 0; t < 12; t += 4) {
                 for (int k = 0; k < 3; ++k) {
@@ -543,20 +570,24 @@ __global__ void __launch_bounds__(kBlock) k_combine(const NodeRec* __restrict__ 
                 for (int k = 0; k < 3; ++k) col[t + k] += rr[t + k];
         }
     }
-    double* dst = nr.parent >= 0 ? parent_child + 24 * (int64_t)nr.parent + 12 * nr.slot : sample_out + 12 * i;
-    if (nr.parent >= 0 && nr.material < 0) return;  // a missed child leaves its zeroed slot
-    for (int k = 0; k < 12; ++k) dst[k] = col[k];
+    if (nr.parent >= 0) {
+        tri_store(parent_child, 2 * (int64_t)nr.parent + nr.slot, col);  // a missed child writes its zeros
+    } else {
+        tri_store(sample_out, (i % spp) * (n / spp) + i / spp, col);
+    }
 }
 
 // pixel_multi_sample + render_multi_helper's (A+D+S)/3 (renderer.c:132-181, 216-233)
-__global__ void __launch_bounds__(kBlock) k_resolve(const double* __restrict__ sample_col, int64_t npix, int32_t spp,
+__global__ void __launch_bounds__(kBlock) k_resolve(Cols<Tri9> sample_col, int64_t npix, int32_t spp,
                                                     double* __restrict__ out) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
     double acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const double* s = sample_col + 12 * p * spp;
-    for (int k = 0; k < spp; ++k)
-        for (int c = 0; c < 12; ++c) acc[c] += s[12 * k + c];
+    for (int k = 0; k < spp; ++k) {  // sub-sample k of pixel p at k * npix + p (k_combine)
+        double s[12];
+        tri_load(sample_col, (int64_t)k * npix + p, s);
+        for (int c = 0; c < 12; ++c) acc[c] += s[c];
+    }
     const double total = (double)spp;
     for (int c = 0; c < 12; ++c) acc[c] *= 1.0 / total;
     double* o = out + 4 * p;
@@ -643,6 +674,7 @@ __global__ void __launch_bounds__(kBlock) k_photon_emit(DevScene S, uint64_t see
 }
 
 // power_at's hit half + photon_hit (photon_tracer.c:114-182) for one bounce
+template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed, int map, int depth,
                                                        const QueuedRay* __restrict__ q, const double* __restrict__ power,
                                                        int64_t n, const HitRec* __restrict__ hits,
@@ -664,17 +696,18 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
     if (pp[0] <= 0 && pp[1] <= 0 && pp[2] <= 0) return;  // shadow / dead photons
     Hit h{hr.t, -1, -1, hr.node};
     Comps c;
-    prepare(S, r, h, c);
+    prepare<kPat>(S, r, h, c);
     c.n1 = hr.n1;
     c.n2 = hr.n2;
     const frt_material& M = S.materials[c.material];
     const bool had_diffuse = (qr.slot & 1) != 0, had_specular = (qr.slot & 2) != 0;
     const uint64_t e = qr.key;
     const double avg_d = (c.Kd[0] + c.Kd[1] + c.Kd[2]) / 3.0;
-    if (any_positive(c.Kd)) {
-        const bool store_it = map == 0 ? had_specular : had_diffuse;
+    const bool store_it = any_positive(c.Kd) && (map == 0 ? had_specular : had_diffuse);
+    const unsigned long long at_store = wave_append(store_count, store_it);
+    {
         if (store_it) {
-            const unsigned long long at = atomicAdd(store_count, 1ull);
+            const unsigned long long at = at_store;
             if ((int64_t)at < store_cap) {
                 StoredPhoton sp;
                 for (int k = 0; k < 3; ++k) {
@@ -705,11 +738,12 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
         if (rr * total < avg_s) choice = 1;
         else if (rr * total < avg_s + avg_t) choice = 2;
     }
-    if (choice < 0) return;
+    bool emit = choice >= 0;  // every lane reaches the queue append below (wave_append)
     QueuedRay nq;
     double np[3];
     int flags = qr.slot;
-    if (choice == 0) {  // reflect_photon_diffuse (photon_tracer.c:31-62)
+    if (!emit) {
+    } else if (choice == 0) {  // reflect_photon_diffuse (photon_tracer.c:31-62)
         for (int k = 0; k < 3; ++k) np[k] = c.Kd[k] * pp[k];
         double nt[3], nb[3], d[3];
         coordinate_system(c.normalv, nt, nb);
@@ -721,7 +755,7 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
         }
         flags |= 1;
     } else if (choice == 1) {  // reflect_photon_specular (photon_tracer.c:64-77)
-        if (!M.reflective) return;
+        emit = M.reflective != 0;
         const double sc = 1.0 / avg_s;
         for (int k = 0; k < 3; ++k) {
             np[k] = pp[k] * sc;
@@ -730,11 +764,11 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
         }
         flags |= 2;
     } else {  // refract_photon (photon_tracer.c:81-112)
-        if (feq(M.Tr, 0.0)) return;
+        emit = !feq(M.Tr, 0.0);
         const double n_ratio = c.n1 / c.n2;
         const double cos_i = dot3(c.eyev, c.normalv);
         const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
-        if (sin2_t > 1.0) return;
+        emit = emit && !(sin2_t > 1.0);
         const double cos_t = sqrt(1.0 - sin2_t);
         const double s1 = n_ratio * cos_i - cos_t;
         const double sc = 1.0 / avg_t;
@@ -747,7 +781,8 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
         }
         flags |= 2;
     }
-    const unsigned long long at = atomicAdd(next_count, 1ull);
+    const unsigned long long at = wave_append(next_count, emit);
+    if (!emit) return;
     if ((int64_t)at >= next_cap) {
         atomicOr(err, kErrQueueOverflow);
         return;
@@ -771,13 +806,13 @@ __device__ inline void photon_estimate(const PhotonMapDev& M, const DevScene& S,
 }
 
 // per shaded node: the visualisation term (lighting_gi) and the caustics term (renderer.c:740-761)
-__global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, const NodeRec* __restrict__ rec, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, Cols<NodeRec> rec, int64_t n,
                                                     double* __restrict__ gi_extra) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double* out = gi_extra + 6 * i;
     for (int k = 0; k < 6; ++k) out[k] = 0.0;
-    const NodeRec& nr = rec[i];
+    const NodeRec nr = rec.load(i);
     if (nr.material < 0 || !any_positive(nr.Kd)) return;
     const double edn = dot3(nr.eyev, nr.normalv);
     if (S.cfg.visualize_photon_map) {  // lighting_gi, visualize branch: the raw estimate
@@ -801,14 +836,14 @@ __global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, const NodeRec* _
 
 // final_gather's rays (renderer.c:648-687): gu x gv cosine-weighted hemisphere
 // directions (a jittered CMJ pattern per gather) from over_point
-__global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed, const NodeRec* __restrict__ rec,
+__global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed, Cols<NodeRec> rec,
                                                        int64_t node0, int64_t nodes, QueuedRay* __restrict__ gq) {
     const int G = S.cfg.gi_usteps * S.cfg.gi_vsteps;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nodes * G) return;
     const int64_t node = node0 + t / G;
     const int slot = (int)(t % G);
-    const NodeRec& nr = rec[node];
+    const NodeRec nr = rec.load(node);
     QueuedRay qr;
     qr.key = nr.key;
     qr.slot = slot;
@@ -833,6 +868,7 @@ __global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed
 
 // color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray, scaled by the sample's
 // first coordinate (final_gather: "scale by theta")
+template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_gather_shade(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
                                                          const HitRec* __restrict__ hits, int64_t n,
                                                          double* __restrict__ gather_col) {
@@ -852,13 +888,13 @@ __global__ void __launch_bounds__(kBlock) k_gather_shade(DevScene S, uint64_t se
     const frt_material& M = S.materials[S.nodes[leaf].material];
     double p[3], diffuse[3];
     for (int k = 0; k < 3; ++k) p[k] = r.o[k] + r.d[k] * hr.t;
-    if (M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, leaf, p, diffuse);
+    if (kPat && M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, leaf, p, diffuse);
     else copy3(M.Kd, diffuse);
     double c[3] = {0, 0, 0};
     if (any_positive(diffuse)) {
         Hit h{hr.t, -1, -1, leaf};
         Comps cp;
-        prepare(S, r, h, cp);
+        prepare<kPat>(S, r, h, cp);
         if (any_positive(cp.Kd)) {  // lighting_gi (renderer.c:863-892)
             double est[3];
             photon_estimate(S.pmaps[1], S, cp.over_point, cp.eyev, 10.0 * (double)S.cfg.irradiance_num, est);
@@ -881,14 +917,14 @@ __global__ void __launch_bounds__(kBlock) k_gather_shade(DevScene S, uint64_t se
 }
 
 // final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd
-__global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, const NodeRec* __restrict__ rec, int64_t node0,
+__global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, Cols<NodeRec> rec, int64_t node0,
                                                           int64_t nodes, const double* __restrict__ gather_col,
                                                           double* __restrict__ fgather) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nodes) return;
     const int64_t node = node0 + t;
     const int G = S.cfg.gi_usteps * S.cfg.gi_vsteps;
-    const NodeRec& nr = rec[node];
+    const NodeRec nr = rec.load(node);
     double* out = fgather + 3 * node;
     out[0] = out[1] = out[2] = 0.0;
     if (nr.material < 0 || !any_positive(nr.Kd)) return;
@@ -900,14 +936,15 @@ __global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, const Node
 }
 
 // shade_hit's GI block (renderer.c:727-770): ambient += indirect, final gather, caustics; clamp to sqrt(3)
-__global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, const NodeRec* __restrict__ rec, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, Cols<NodeRec> rec, int64_t n,
                                                      const double* __restrict__ gi_extra,
-                                                     const double* __restrict__ fgather, double* __restrict__ surface) {
+                                                     const double* __restrict__ fgather, Cols<Tri9> surface) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec& nr = rec[i];
+    const NodeRec nr = rec.load(i);
     if (nr.material < 0 || !any_positive(nr.Kd)) return;
-    double* a = surface + 12 * i;
+    double a[12];
+    tri_load(surface, i, a);
     for (int k = 0; k < 3; ++k) a[k] += gi_extra[6 * i + k];
     if (fgather != nullptr)
         for (int k = 0; k < 3; ++k) a[k] += fgather[3 * i + k];
@@ -917,6 +954,7 @@ __global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, const NodeRec* 
         for (int k = 0; k < 3; ++k) a[k] *= 1.0 / len;
         for (int k = 0; k < 3; ++k) a[k] *= 1.7320508075688772;
     }
+    tri_store(surface, i, a);
 }
 
 }  // namespace frt
@@ -942,22 +980,26 @@ struct frt_scene_handle {
     unsigned redo_cap = 0;
     // work buffers (grow on demand)
     struct Level {
-        frt::NodeRec* rec = nullptr;
+        frt::Cols<frt::NodeRec> rec;
         frt::ShadowHead* head = nullptr;
         frt::QueuedRay* q = nullptr;
-        double* surface = nullptr;
-        double* child = nullptr;
+        frt::Cols<frt::Tri9> surface;
+        frt::Cols<frt::Tri9> child;  // two slots per node: 2 i (reflected), 2 i + 1 (refracted)
+        int64_t* qprefix = nullptr;                     // queue segments of this level (frt_shadow.hpp)
+        std::vector<int64_t> hprefix = std::vector<int64_t>(frt::kQueueSegs + 1, 0);
         int32_t* counts = nullptr;
         int64_t cap = 0;
     };
     std::vector<Level> levels;
     frt::HitRec* hits = nullptr;  // closest hits of the level being traced
     int64_t hits_cap = 0;
-    double* sample_col = nullptr;
+    frt::Cols<frt::Tri9> sample_col;
     int64_t sample_cap = 0;
     double* out_dev = nullptr;
     int64_t out_cap = 0;
-    unsigned long long* counters = nullptr;  // [0..15] queue counts per level, [16] pruned
+    // kQueueSegs lines of kCounterLine words: [d] queue segment count of level d, [16] pruned,
+    // [17] shaded path nodes (per segment); line 0 [24] / [25]: photon store / photon queue
+    unsigned long long* counters = nullptr;
     unsigned* err = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     struct Mark {
@@ -1303,7 +1345,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         return fail("frt_scene_upload: debug counters");
     }
 #endif
-    if (hipStreamCreate(&h->stream) != hipSuccess || hipMalloc((void**)&h->counters, 32 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipStreamCreate(&h->stream) != hipSuccess || hipMalloc((void**)&h->counters, frt::kQueueSegs * frt::kCounterLine * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&h->err, sizeof(unsigned)) != hipSuccess || hipEventCreate(&h->ev[0]) != hipSuccess ||
         hipEventCreate(&h->ev[1]) != hipSuccess) {
         frt_scene_release(h);
@@ -1319,12 +1361,13 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipSetDevice(h->device));
     for (void* p : h->owned) hip_ignore(hipFree(p));
     for (auto& L : h->levels) {
-        hip_ignore(hipFree(L.rec));
+        hip_ignore(hipFree(L.rec.w));
         hip_ignore(hipFree(L.head));
         hip_ignore(hipFree(L.q));
-        hip_ignore(hipFree(L.surface));
-        hip_ignore(hipFree(L.child));
+        hip_ignore(hipFree(L.surface.w));
+        hip_ignore(hipFree(L.child.w));
         hip_ignore(hipFree(L.counts));
+        hip_ignore(hipFree(L.qprefix));
     }
     hip_ignore(hipFree(h->hits));
     {
@@ -1342,7 +1385,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(G.extra));
         hip_ignore(hipFree(G.fgather));
     }
-    hip_ignore(hipFree(h->sample_col));
+    hip_ignore(hipFree(h->sample_col.w));
     hip_ignore(hipFree(h->out_dev));
     hip_ignore(hipFree(h->counters));
     hip_ignore(hipFree(h->err));
@@ -1357,23 +1400,27 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     auto& L = h->levels[d];
     if (need <= L.cap) return 0;
     int64_t nc = std::max<int64_t>(need, L.cap * 2);
-    hip_ignore(hipFree(L.rec));
+    hip_ignore(hipFree(L.rec.w));
     hip_ignore(hipFree(L.head));
     L.head = nullptr;
     hip_ignore(hipFree(L.q));
-    hip_ignore(hipFree(L.surface));
-    hip_ignore(hipFree(L.child));
+    hip_ignore(hipFree(L.surface.w));
+    hip_ignore(hipFree(L.child.w));
     hip_ignore(hipFree(L.counts));
-    L.rec = nullptr;
+    L.rec = {};
     L.q = nullptr;
-    L.surface = nullptr;
-    L.child = nullptr;
+    L.surface = {};
+    L.child = {};
     L.counts = nullptr;
-    FRT_HIP(hipMalloc((void**)&L.rec, nc * sizeof(frt::NodeRec)));
+    FRT_HIP(hipMalloc((void**)&L.rec.w, frt::Cols<frt::NodeRec>::bytes(nc)));
+    L.rec.cap = nc;
     FRT_HIP(hipMalloc((void**)&L.head, nc * sizeof(frt::ShadowHead)));
     FRT_HIP(hipMalloc((void**)&L.q, nc * sizeof(frt::QueuedRay)));
-    FRT_HIP(hipMalloc((void**)&L.surface, nc * 12 * sizeof(double)));
-    FRT_HIP(hipMalloc((void**)&L.child, nc * 24 * sizeof(double)));
+    FRT_HIP(hipMalloc((void**)&L.surface.w, frt::Cols<frt::Tri9>::bytes(nc)));
+    L.surface.cap = nc;
+    FRT_HIP(hipMalloc((void**)&L.child.w, frt::Cols<frt::Tri9>::bytes(2 * nc)));
+    L.child.cap = 2 * nc;
+    if (!L.qprefix) FRT_HIP(hipMalloc((void**)&L.qprefix, (frt::kQueueSegs + 1) * sizeof(int64_t)));
     FRT_HIP(hipMalloc((void**)&L.counts, nc * std::max(1, h->S.num_lights) * sizeof(int32_t)));
     L.cap = nc;
     return 0;
@@ -1537,7 +1584,7 @@ static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t
             FRT_HIP(hipMemsetAsync(next_count, 0, sizeof(unsigned long long), h->stream));
             launch_trace(h, B, G.pq[cur], n, G.phits, 1);
             FRT_HIP(hipGetLastError());
-            hipLaunchKernelGGL(k_photon_hit, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, lseed, map, depth,
+            hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_photon_hit<true> : k_photon_hit<false>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, lseed, map, depth,
                                G.pq[cur], G.ppow[cur], n, G.phits, G.pq[cur ^ 1], G.ppow[cur ^ 1], next_count,
                                batch, G.store, store_count, store_cap, h->err);
             FRT_HIP(hipGetLastError());
@@ -1691,8 +1738,10 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
                 return -1;
             hipLaunchKernelGGL(k_gather_gen, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, L.rec, n0, m,
                                G.gq);
-            launch_trace(h, B, G.gq, rays, G.ghits, 0);
-            hipLaunchKernelGGL(k_gather_shade, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq,
+            frt::Batch Bg = B;  // the gather rays form one contiguous queue
+            Bg.qprefix = nullptr;
+            launch_trace(h, Bg, G.gq, rays, G.ghits, 0);
+            hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_gather_shade<true> : k_gather_shade<false>, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq,
                                G.ghits, rays, G.gcol);
             hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
                                G.fgather);
@@ -1732,6 +1781,9 @@ static void dump_walk_stats(frt_scene_handle* h) {
     std::fprintf(stderr, "walk prof (shadow, cycles):");
     const char* pn[8] = {"setup", "close", "xf_pop", "composite", "leaf_xf", "leaf_test", "leaf_post", "loop"};
     for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s=%llu", pn[k], c[frt::kDbgProf + k]);
+    std::fprintf(stderr, "\nprepare prof (cycles):");
+    const char* qn[5] = {"ray", "hits_load", "prepare", "spawn", "stores"};
+    for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s=%llu", qn[k], c[frt::kDbgProf + 8 + k]);
     std::fprintf(stderr, "\n");
 }
 #endif
@@ -1754,7 +1806,7 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         (void)hipEventRecord(h->ev[0], h->stream);
     }
     FRT_HIP(hipMemsetAsync(h->err, 0, sizeof(unsigned), h->stream));
-    FRT_HIP(hipMemsetAsync(h->counters, 0, 32 * sizeof(unsigned long long), h->stream));
+    FRT_HIP(hipMemsetAsync(h->counters, 0, frt::kQueueSegs * frt::kCounterLine * sizeof(unsigned long long), h->stream));
     if (h->S.cfg.use_gi && (!h->gi.built || h->gi.seed != P->seed)) {
         // the photon maps belong to the render seed: same seed, same image (also across row splits)
         hipEvent_t p0 = nullptr, p1 = nullptr;
@@ -1779,13 +1831,19 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         st->photons[0] = h->gi.photons[0];
         st->photons[1] = h->gi.photons[1];
     }
-    unsigned long long host_counters[32];
+    std::vector<unsigned long long> host_counters((size_t)kQueueSegs * kCounterLine);
     for (int64_t p0 = 0; p0 < npix; p0 += pix_per_batch) {
         const int64_t bp = std::min<int64_t>(pix_per_batch, npix - p0);
         const int64_t ns = bp * spp;
-        if (grow(&h->sample_col, h->sample_cap, ns * 12)) return -1;
+        if (ns > h->sample_cap) {
+            hip_ignore(hipFree(h->sample_col.w));
+            h->sample_col = {};
+            h->sample_cap = 0;
+            FRT_HIP(hipMalloc((void**)&h->sample_col.w, frt::Cols<frt::Tri9>::bytes(ns)));
+            h->sample_col.cap = h->sample_cap = ns;
+        }
         if (ensure_level(h, 0, ns)) return -1;
-        Batch B;
+        Batch B{};
         B.sample_begin = 0;
         // global sample index of the first sample: pixel (row, col) in frame coordinates
         const int64_t first_row = P->row_begin + (p0 / hs) * stride;
@@ -1798,16 +1856,21 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         B.spp = spp;
         std::vector<int64_t> count(path + 2, 0);
         count[0] = ns;
-        FRT_HIP(hipMemsetAsync(h->counters, 0, 16 * sizeof(unsigned long long), h->stream));
+        // the queue counts (words 0..15) of every counter line
+        FRT_HIP(hipMemset2DAsync(h->counters, kCounterLine * sizeof(unsigned long long), 0, 16 * sizeof(unsigned long long),
+                                 kQueueSegs, h->stream));
         for (int d = 0; d <= path; ++d) {
             const int64_t n = count[d];
             if (n == 0) break;
             B.level = d;
             B.remaining = path - d;
             auto& L = h->levels[d];
-            if (ensure_level(h, d + 1, std::max<int64_t>(2 * n, 1024))) return -1;
+            // a block appends up to 2 * kBlock rays to its segment: 2n plus one block's worth per segment
+            if (ensure_level(h, d + 1, 2 * n + (int64_t)kQueueSegs * 2 * kBlock)) return -1;
             auto& N = h->levels[d + 1];
-            FRT_HIP(hipMemsetAsync(L.child, 0, (size_t)n * 24 * sizeof(double), h->stream));
+            B.qprefix = d > 0 ? L.qprefix : nullptr;
+            B.qsegcap = L.cap / kQueueSegs;
+            B.next_segcap = N.cap / kQueueSegs;
             FRT_HIP(hipMemsetAsync(L.counts, 0, (size_t)n * std::max(1, h->S.num_lights) * sizeof(int32_t), h->stream));
             if (grow(&h->hits, h->hits_cap, n)) return -1;
             const QueuedRay* q = d == 0 ? nullptr : L.q;
@@ -1818,8 +1881,9 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
             }
             {
                 KTimer t(h, st, 6);
-                hipLaunchKernelGGL(k_prepare, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
-                                   L.rec, L.head, N.q, N.cap, h->counters + d + 1, h->counters + 16, h->err);
+                hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
+                                   dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
+                                   L.rec, L.head, N.q, h->counters, h->err);
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.include_direct && h->samples_per_node > 0) {
@@ -1837,15 +1901,29 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
                 KTimer t(h, st, 7);
                 if (shade_gi(h, B, L, n, st)) return -1;
             }
-            FRT_HIP(hipMemcpyAsync(host_counters, h->counters, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                   h->stream));
+            FRT_HIP(hipMemcpyAsync(host_counters.data(), h->counters, host_counters.size() * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, h->stream));
             FRT_HIP(hipStreamSynchronize(h->stream));
-            int64_t next = (int64_t)host_counters[d + 1];
-            if (next > N.cap) {
+            // the next level's queue segments: prefix counts (a segment past its capacity is an error)
+            int64_t next = 0;
+            bool overflow = false;
+            for (int j = 0; j < kQueueSegs; ++j) {
+                N.hprefix[j] = next;
+                int64_t c = (int64_t)host_counters[(size_t)j * kCounterLine + d + 1];
+                if (c > B.next_segcap) {
+                    overflow = true;
+                    c = B.next_segcap;
+                }
+                next += c;
+            }
+            N.hprefix[kQueueSegs] = next;
+            if (overflow) {
                 unsigned e = kErrQueueOverflow;
                 FRT_HIP(hipMemcpyAsync(h->err, &e, sizeof(unsigned), hipMemcpyHostToDevice, h->stream));
-                next = N.cap;
             }
+            if (next > 0 && d < path)
+                FRT_HIP(hipMemcpyAsync(N.qprefix, N.hprefix.data(), (kQueueSegs + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
+                                       h->stream));
             count[d + 1] = d < path ? next : 0;
             if (st) {
                 if (d > 0) st->secondary_rays += (uint64_t)n;
@@ -1856,10 +1934,10 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
             const int64_t n = count[d];
             if (n == 0) continue;
             KTimer t(h, st, 3);
-            double* parent_child = d > 0 ? h->levels[d - 1].child : nullptr;
+            const Cols<Tri9> parent_child = d > 0 ? h->levels[d - 1].child : Cols<Tri9>{};
             hipLaunchKernelGGL(k_combine, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->levels[d].rec, n,
-                               h->levels[d].surface, h->levels[d].child, parent_child, h->sample_col, h->S.materials,
-                               h->S.cfg.include_specular);
+                               h->levels[d].surface, h->levels[d].child, parent_child, h->sample_col, spp,
+                               h->S.materials, h->S.cfg.include_specular);
             FRT_HIP(hipGetLastError());
         }
         {
@@ -1869,7 +1947,8 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
             FRT_HIP(hipGetLastError());
         }
     }
-    FRT_HIP(hipMemcpyAsync(host_counters, h->counters, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+    FRT_HIP(hipMemcpyAsync(host_counters.data(), h->counters, host_counters.size() * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, h->stream));
     unsigned err = 0;
     FRT_HIP(hipMemcpyAsync(&err, h->err, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
     if (st) (void)hipEventRecord(h->ev[1], h->stream);
@@ -1878,12 +1957,17 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
         st->render_ms = ms;
-        st->pruned_secondary = host_counters[16];
-        st->hits = host_counters[17];
-        st->shadow_rays = h->S.cfg.include_direct ? host_counters[17] * (uint64_t)h->samples_per_node : 0;
+        uint64_t pruned = 0, hits = 0;
+        for (int j = 0; j < kQueueSegs; ++j) {
+            pruned += host_counters[(size_t)j * kCounterLine + 16];
+            hits += host_counters[(size_t)j * kCounterLine + 17];
+        }
+        st->pruned_secondary = pruned;
+        st->hits = hits;
+        st->shadow_rays = h->S.cfg.include_direct ? hits * (uint64_t)h->samples_per_node : 0;
         // DESIGN.md byte model: per shaded node its 64-byte ShadowHead read + one 4-byte count per light written
         st->shadow_kernel_bytes =
-            h->S.cfg.include_direct && h->samples_per_node > 0 ? (double)host_counters[17] * (64.0 + 4.0 * h->S.num_lights) : 0.0;
+            h->S.cfg.include_direct && h->samples_per_node > 0 ? (double)hits * (64.0 + 4.0 * h->S.num_lights) : 0.0;
         st->errors = err;
         st->shadow_jit = h->jit_shadow != nullptr ? 1 : 0;
         collect_timings(h, st);

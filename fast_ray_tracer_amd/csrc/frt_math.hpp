@@ -178,6 +178,30 @@ __device__ __forceinline__ bool box_decide(const double* bb, const Ray& r, const
     return box_range(bb, r, a, b);
 }
 
+// ---- wave-aggregated counters ----
+// One atomic per wave instead of one per lane: a single shared counter taking
+// an atomic from every path node serialises at its L2 channel (the queue
+// appends of k_prepare cost more than the rest of the kernel). Every active
+// lane of the wave must call it at the same point; returns this lane's slot
+// (base + rank among the lanes with want), meaningless where want is false.
+__device__ __forceinline__ unsigned long long wave_append(unsigned long long* ctr, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0) return 0;
+    const int leader = __builtin_ctzll(m);
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)base, leader);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(base >> 32), leader);
+    return (((unsigned long long)hi << 32) | lo) + (unsigned long long)__popcll(m & ((1ull << lane) - 1));
+}
+
+// statistics counter: one atomic per wave whose result nobody waits for
+__device__ __forceinline__ void wave_count(unsigned long long* ctr, bool cond) {
+    const unsigned long long m = __ballot(cond);
+    if (m != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(ctr, (unsigned long long)__popcll(m));
+}
+
 // ---- binary32 box decisions with a rigorous error bound ----
 // The reference decides a box hit as tmin <= tmax over binary64 slab quotients
 // (lo - o) / d (bounding_box.c:124-175). Here the quotients come from binary32

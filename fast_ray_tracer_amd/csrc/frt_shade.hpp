@@ -420,13 +420,16 @@ struct Comps {
     int leaf, material;
 };
 
+// kPat = false: the scene has no patterns (every map_* is -1), so the pattern
+// code — most of prepare's registers and its scratch — is compiled out
+template <bool kPat = true>
 __device__ inline void normal_at(const DevScene& S, int leaf, const double* wp, const Hit& h, double* n) {
     double lp[3], ln[3];
     world_to_object(S, leaf, wp, lp);
     local_normal(S, leaf, lp, h, ln);
     normal_to_world(S, leaf, ln);
     const frt_material& M = S.materials[S.nodes[leaf].material];
-    if (M.map_bump >= 0) {
+    if (kPat && M.map_bump >= 0) {
         double tmp[3];
         pattern_at_shape<kPatternDepth>(S, M.map_bump, leaf, wp, tmp);
         for (int k = 0; k < 3; ++k) {
@@ -437,6 +440,7 @@ __device__ inline void normal_at(const DevScene& S, int leaf, const double* wp, 
     normalize3(ln, n);
 }
 
+template <bool kPat = true>
 __device__ inline void prepare(const DevScene& S, const Ray& r, Hit h, Comps& c) {
     if (S.nodes[h.node].type == FRT_TRIANGLE || S.nodes[h.node].type == FRT_SMOOTH_TRIANGLE) {
         // the walk keeps (t, node) only; the triangle's (u, v) are recomputed with the same ray
@@ -451,7 +455,7 @@ __device__ inline void prepare(const DevScene& S, const Ray& r, Hit h, Comps& c)
     c.leaf = h.node;
     c.material = S.nodes[h.node].material;
     for (int k = 0; k < 3; ++k) c.p[k] = r.o[k] + r.d[k] * h.t;
-    normal_at(S, h.node, c.p, h, c.normalv);
+    normal_at<kPat>(S, h.node, c.p, h, c.normalv);
     for (int k = 0; k < 3; ++k) c.eyev[k] = r.d[k] * -1.0;
     if (dot3(c.normalv, c.eyev) < 0) {
         for (int k = 0; k < 3; ++k) c.normalv[k] *= -1;
@@ -465,22 +469,22 @@ __device__ inline void prepare(const DevScene& S, const Ray& r, Hit h, Comps& c)
     c.n1 = 1.0;
     c.n2 = 1.0;
     const frt_material& M = S.materials[c.material];
-    if (M.map_Ka >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Ka, c.leaf, c.over_point, c.Ka);
+    if (kPat && M.map_Ka >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Ka, c.leaf, c.over_point, c.Ka);
     else copy3(M.Ka, c.Ka);
-    if (M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, c.leaf, c.over_point, c.Kd);
+    if (kPat && M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, c.leaf, c.over_point, c.Kd);
     else copy3(M.Kd, c.Kd);
-    if (M.map_Ks >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Ks, c.leaf, c.over_point, c.Ks);
+    if (kPat && M.map_Ks >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Ks, c.leaf, c.over_point, c.Ks);
     else copy3(M.Ks, c.Ks);
-    if (M.map_refl >= 0) pattern_at_shape<kPatternDepth>(S, M.map_refl, c.leaf, c.over_point, c.refl);
+    if (kPat && M.map_refl >= 0) pattern_at_shape<kPatternDepth>(S, M.map_refl, c.leaf, c.over_point, c.refl);
     else copy3(M.refl, c.refl);
-    if (M.map_Ns >= 0) {
+    if (kPat && M.map_Ns >= 0) {
         double tmp[3];
         pattern_at_shape<kPatternDepth>(S, M.map_Ns, c.leaf, c.over_point, tmp);
         c.Ns = tmp[0];
     } else {
         c.Ns = M.Ns;
     }
-    if (M.map_d >= 0) {
+    if (kPat && M.map_d >= 0) {
         double tmp[3];
         pattern_at_shape<kPatternDepth>(S, M.map_d, c.leaf, c.over_point, tmp);
         c.over_d = tmp[0];

@@ -26,6 +26,14 @@ __device__ __forceinline__ int light_row(const frt_light& L, uint64_t seed, uint
     return (int)(h % (uint64_t)L.rows);
 }
 
+// Ray queues of the levels are segmented: a block appends to segment
+// blockIdx % kQueueSegs through that segment's own counter (one per 256-byte
+// line), because device-scope atomics on one address serialise (~12 ns each:
+// tools/microbench/atomics.hip). Segment j of a level's queue holds entries
+// [qprefix[j], qprefix[j+1]) of the level at j * qsegcap + (i - qprefix[j]).
+constexpr int kQueueSegs = 64;
+constexpr int kCounterLine = 32;  // 8-byte words per counter line (256 bytes)
+
 struct Batch {
     int64_t sample_begin;  // first global sample index of the batch
     int64_t pixel_begin;   // first pixel (in render order) of the batch
@@ -34,7 +42,23 @@ struct Batch {
     uint64_t seed;
     int32_t spp, level;
     int32_t remaining;     // path_length - level
+    int32_t pad;
+    const int64_t* qprefix;  // this level's queue segments (kQueueSegs + 1 prefix counts); null: contiguous
+    int64_t qsegcap;         // entries per segment of this level's queue
+    int64_t next_segcap;     // entries per segment of the next level's queue
 };
+
+// storage slot of entry i of the level's queue
+__device__ __forceinline__ int64_t queue_slot(const Batch& B, int64_t i) {
+    if (B.qprefix == nullptr) return i;
+    int lo = 0, hi = kQueueSegs;  // the last segment j with qprefix[j] <= i
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (B.qprefix[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return (int64_t)lo * B.qsegcap + (i - B.qprefix[lo]);
+}
 
 // what k_shadow reads of a path node, one 64-byte line per node (the shadow
 // pass re-reads it from 100 lanes; keeping it apart from the 216-byte NodeRec

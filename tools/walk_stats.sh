@@ -8,5 +8,5 @@ cp exp/stats.so fast_ray_tracer_amd/lib/libfrt_device.so
 timeout -k 10 200 python bench.py --steps 1 --warmup 0 --no-cpu-baseline --scene $SCENE > gpurun_out/stats_$SCENE.json 2> gpurun_out/stats_$SCENE.err
 rc=$?
 cp /tmp/frt_base.so fast_ray_tracer_amd/lib/libfrt_device.so
-grep -E "walk stats|node visits|walk prof" gpurun_out/stats_$SCENE.err
+grep -E "walk stats|node visits|walk prof|prepare prof" gpurun_out/stats_$SCENE.err
 exit $rc
