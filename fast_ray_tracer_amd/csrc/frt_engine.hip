@@ -463,41 +463,51 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<Node
             for (int k = 0; k < 3; ++k) amb[k] = nr.Ka[k] * L.intensity[k];
             if (!feq(inten, 0.0)) {
                 if (S.cfg.include_diffuse || S.cfg.include_spec_highlight) {
-                    const int row = light_row(L, B.seed, nr.key, li, 1);
-                    const double* pts = S.light_points + L.points + 3 * (int64_t)row * L.num_samples;
                     double ned = 0.0;
                     if (S.cfg.include_spec_highlight) ned = dot3(nr.normalv, nr.eyev);
                     double dacc[3] = {0, 0, 0}, sacc[3] = {0, 0, 0};
-                    for (int p = 0; p < L.num_samples; ++p) {
-                        const double* lp = pts + 3 * p;
-                        double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
-                        double lv[3];
-                        normalize3(diff, lv);
-                        double ldn = dot3(lv, nr.normalv);
-                        if (S.cfg.include_diffuse && ldn >= 0.0) {
-                            for (int k = 0; k < 3; ++k) {
-                                double cc = nr.Kd[k] * L.intensity[k];
-                                cc *= ldn;
-                                dacc[k] += cc;
+                    auto points = [&](const double* pts) {
+                        for (int p = 0; p < L.num_samples; ++p) {
+                            const double* lp = pts + 3 * p;
+                            double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
+                            double lv[3];
+                            normalize3(diff, lv);
+                            double ldn = dot3(lv, nr.normalv);
+                            if (S.cfg.include_diffuse && ldn >= 0.0) {
+                                for (int k = 0; k < 3; ++k) {
+                                    double cc = nr.Kd[k] * L.intensity[k];
+                                    cc *= ldn;
+                                    dacc[k] += cc;
+                                }
+                            }
+                            if (S.cfg.include_spec_highlight && ldn >= 0.0) {
+                                double ndl = dot3(nr.normalv, lv);
+                                double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
+                                normalize3(tmp, hv);
+                                double ndh = fmax(0.0, dot3(nr.normalv, hv));
+                                double edh_inv = 1.0 / fmax(0.0, dot3(nr.eyev, hv));
+                                double ldh = dot3(lv, hv);
+                                double dist_term = (nr.Ns + 2) * pow(ndh, nr.Ns) * 0.5 * k1Pi;
+                                double gc = 2.0 * ndh * edh_inv;
+                                double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
+                                // pow(1 - ldh, 5.0) (renderer.c:969) by squaring: within an ulp or two of the
+                                // reference's libm pow, like the device pow it replaces
+                                const double om = 1.0 - ldh, om2 = om * om;
+                                double factor = om2 * om2 * om;
+                                double brdf = dist_term * geo / (4.0 * ndl * ned);
+                                for (int k = 0; k < 3; ++k) {
+                                    double f = nr.Ks[k] + (1.0 - nr.Ks[k]) * factor;
+                                    sacc[k] += f * L.intensity[k] * brdf;
+                                }
                             }
                         }
-                        if (S.cfg.include_spec_highlight && ldn >= 0.0) {
-                            double ndl = dot3(nr.normalv, lv);
-                            double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
-                            normalize3(tmp, hv);
-                            double ndh = fmax(0.0, dot3(nr.normalv, hv));
-                            double edh_inv = 1.0 / fmax(0.0, dot3(nr.eyev, hv));
-                            double ldh = dot3(lv, hv);
-                            double dist_term = (nr.Ns + 2) * pow(ndh, nr.Ns) * 0.5 * k1Pi;
-                            double gc = 2.0 * ndh * edh_inv;
-                            double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
-                            double factor = pow(1.0 - ldh, 5.0);
-                            double brdf = dist_term * geo / (4.0 * ndl * ned);
-                            for (int k = 0; k < 3; ++k) {
-                                double f = nr.Ks[k] + (1.0 - nr.Ks[k]) * factor;
-                                sacc[k] += f * L.intensity[k] * brdf;
-                            }
-                        }
+                    };
+                    const double* row0 = S.light_points + L.points;
+                    if (L.rows <= 1) {
+                        points(row0);  // one cache row: the same points in every lane, through the scalar cache
+                    } else {
+                        const int row = light_row(L, B.seed, nr.key, li, 1);
+                        points(row0 + 3 * (int64_t)row * L.num_samples);
                     }
                     double scaling = inten / (double)L.num_samples;
                     for (int k = 0; k < 3; ++k) {
