@@ -815,29 +815,66 @@ __device__ inline void photon_estimate(const PhotonMapDev& M, const DevScene& S,
     }
 }
 
+// the wave's LDS for wave_irradiance_estimate (frt_gi.hpp); blocks of kBlock threads
+#define FRT_EST_LDS(name)                                                    \
+    __shared__ float name##_d2[kBlock / 64][kEstCap];                        \
+    __shared__ int32_t name##_idx[kBlock / 64][kEstCap];                     \
+    __shared__ unsigned name##_hist[kBlock / 64][256];                       \
+    const EstLds name{name##_d2[threadIdx.x >> 6], name##_idx[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6]}
+
+// the lanes' estimate requests one after another, each by the whole wave; every lane of the
+// wave must call this at the same point. est: this lane's scaled estimate (photon_estimate)
+__device__ inline void wave_photon_estimates(const PhotonMapDev& M, const DevScene& S, bool want, const double* point,
+                                             const double* eyev, double scale_num, double* est, const EstLds& L) {
+    est[0] = est[1] = est[2] = 0.0;
+    unsigned long long reqs = __ballot(want);
+    while (reqs) {
+        const int j = __builtin_ctzll(reqs);
+        reqs &= reqs - 1;
+        double x[3], nrm[3], e[3];
+        for (int k = 0; k < 3; ++k) {
+            x[k] = __shfl(point[k], j, 64);
+            nrm[k] = __shfl(eyev[k], j, 64);
+        }
+        // the reference passes eyev as the estimate's normal (renderer.c:875)
+        const int64_t used = wave_irradiance_estimate(M, x, nrm, S.cfg.irradiance_radius, S.cfg.irradiance_num,
+                                                      S.cfg.cone_filter_k, e, L);
+        if (est_lane() == j && used > 0) {
+            const double f = scale_num / (double)used;
+            for (int k = 0; k < 3; ++k) est[k] = e[k] * f;
+        }
+    }
+}
+
 // per shaded node: the visualisation term (lighting_gi) and the caustics term (renderer.c:740-761)
 __global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, Cols<NodeRec> rec, int64_t n,
                                                     double* __restrict__ gi_extra) {
+    FRT_EST_LDS(lds);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    NodeRec nr{};
+    bool want = false;
+    if (i < n) {
+        nr = rec.load(i);
+        want = nr.material >= 0 && any_positive(nr.Kd);
+    }
+    double vis[3] = {0, 0, 0}, cau[3] = {0, 0, 0};
+    if (S.cfg.visualize_photon_map)  // lighting_gi, visualize branch: the raw estimate
+        wave_photon_estimates(S.pmaps[1], S, want, nr.over_point, nr.eyev, 10.0 * (double)S.cfg.irradiance_num, vis,
+                              lds);
+    if (S.cfg.include_caustics) wave_photon_estimates(S.pmaps[0], S, want, nr.over_point, nr.eyev, 100.0, cau, lds);
     if (i >= n) return;
     double* out = gi_extra + 6 * i;
     for (int k = 0; k < 6; ++k) out[k] = 0.0;
-    const NodeRec nr = rec.load(i);
-    if (nr.material < 0 || !any_positive(nr.Kd)) return;
+    if (!want) return;
     const double edn = dot3(nr.eyev, nr.normalv);
-    if (S.cfg.visualize_photon_map) {  // lighting_gi, visualize branch: the raw estimate
-        double est[3];
-        photon_estimate(S.pmaps[1], S, nr.over_point, nr.eyev, 10.0 * (double)S.cfg.irradiance_num, est);
-        for (int k = 0; k < 3; ++k) out[k] = est[k];
-    }
+    if (S.cfg.visualize_photon_map)
+        for (int k = 0; k < 3; ++k) out[k] = vis[k];
     if (S.cfg.include_caustics) {
-        double est[3];
-        photon_estimate(S.pmaps[0], S, nr.over_point, nr.eyev, 100.0, est);
         if (S.cfg.visualize_photon_map) {
-            for (int k = 0; k < 3; ++k) out[3 + k] = est[k];
+            for (int k = 0; k < 3; ++k) out[3 + k] = cau[k];
         } else {
             for (int k = 0; k < 3; ++k) {
-                double ck = nr.Kd[k] * est[k];
+                double ck = nr.Kd[k] * cau[k];
                 out[3 + k] = 0.0 + ck * edn;
             }
         }
@@ -877,53 +914,67 @@ __global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed
 }
 
 // color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray, scaled by the sample's
-// first coordinate (final_gather: "scale by theta")
+// first coordinate (final_gather: "scale by theta"); the photon estimates wave-cooperatively
 template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_gather_shade(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
                                                          const HitRec* __restrict__ hits, int64_t n,
                                                          double* __restrict__ gather_col) {
+    FRT_EST_LDS(lds);
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    double* out = gather_col + 3 * t;
-    out[0] = out[1] = out[2] = 0.0;
-    const QueuedRay qr = gq[t];
-    const HitRec hr = hits[t];
-    if (qr.parent < 0 || hr.node < 0) return;
-    Ray r;
-    for (int k = 0; k < 3; ++k) {
-        r.o[k] = qr.o[k];
-        r.d[k] = qr.d[k];
-    }
-    const int leaf = hr.node;
-    const frt_material& M = S.materials[S.nodes[leaf].material];
-    double p[3], diffuse[3];
-    for (int k = 0; k < 3; ++k) p[k] = r.o[k] + r.d[k] * hr.t;
-    if (kPat && M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, leaf, p, diffuse);
-    else copy3(M.Kd, diffuse);
-    double c[3] = {0, 0, 0};
-    if (any_positive(diffuse)) {
-        Hit h{hr.t, -1, -1, leaf};
-        Comps cp;
-        prepare<kPat>(S, r, h, cp);
-        if (any_positive(cp.Kd)) {  // lighting_gi (renderer.c:863-892)
-            double est[3];
-            photon_estimate(S.pmaps[1], S, cp.over_point, cp.eyev, 10.0 * (double)S.cfg.irradiance_num, est);
-            if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
-                for (int k = 0; k < 3; ++k) c[k] = est[k] * kPi;  // shade_hit_gi: x pi
-            } else {
-                const double edn = dot3(cp.eyev, cp.normalv);
-                for (int k = 0; k < 3; ++k) {
-                    double dk = cp.Kd[k] * est[k];
-                    dk = dk * edn;
-                    c[k] = dk * kPi;  // shade_hit_gi: x pi
+    bool want = false;
+    double pt[3] = {0, 0, 0}, ev[3] = {0, 0, 0}, kd[3] = {0, 0, 0}, edn = 0.0;
+    QueuedRay qr{};
+    if (t < n) {
+        qr = gq[t];
+        const HitRec hr = hits[t];
+        if (qr.parent >= 0 && hr.node >= 0) {
+            Ray r;
+            for (int k = 0; k < 3; ++k) {
+                r.o[k] = qr.o[k];
+                r.d[k] = qr.d[k];
+            }
+            const int leaf = hr.node;
+            const frt_material& M = S.materials[S.nodes[leaf].material];
+            double p[3], diffuse[3];
+            for (int k = 0; k < 3; ++k) p[k] = r.o[k] + r.d[k] * hr.t;
+            if (kPat && M.map_Kd >= 0) pattern_at_shape<kPatternDepth>(S, M.map_Kd, leaf, p, diffuse);
+            else copy3(M.Kd, diffuse);
+            if (any_positive(diffuse)) {
+                Hit h{hr.t, -1, -1, leaf};
+                Comps cp;
+                prepare<kPat>(S, r, h, cp);
+                if (any_positive(cp.Kd)) {  // lighting_gi (renderer.c:863-892)
+                    want = true;
+                    edn = dot3(cp.eyev, cp.normalv);
+                    for (int k = 0; k < 3; ++k) {
+                        pt[k] = cp.over_point[k];
+                        ev[k] = cp.eyev[k];
+                        kd[k] = cp.Kd[k];
+                    }
                 }
+            }
+        }
+    }
+    double est[3];
+    wave_photon_estimates(S.pmaps[1], S, want, pt, ev, 10.0 * (double)S.cfg.irradiance_num, est, lds);
+    if (t >= n) return;
+    double out3[3] = {0, 0, 0};
+    if (want) {
+        if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
+            for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
+        } else {
+            for (int k = 0; k < 3; ++k) {
+                double dk = kd[k] * est[k];
+                dk = dk * edn;
+                out3[k] = dk * kPi;  // shade_hit_gi: x pi
             }
         }
     }
     double jit[2];
     cmj_point(seed ^ kTagGather, qr.key, S.cfg.gi_usteps, S.cfg.gi_vsteps, qr.slot % S.cfg.gi_usteps,
               qr.slot / S.cfg.gi_usteps, jit);
-    for (int k = 0; k < 3; ++k) out[k] = c[k] * jit[0];
+    double* out = gather_col + 3 * t;
+    for (int k = 0; k < 3; ++k) out[k] = out3[k] * jit[0];
 }
 
 // final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd
@@ -1694,16 +1745,24 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
             dir[3 * j + k] = d[k];
         }
     }
-    const size_t bytes = nd * sizeof(double) + start.size() * sizeof(int32_t);
+    // binary32 positions (x, y, z, 0) for the estimate's candidate scan (frt_gi.hpp)
+    std::vector<float> pos4((size_t)std::max<int64_t>(n, 1) * 4, 0.0f);
+    for (int64_t j = 0; j < n; ++j)
+        for (int k = 0; k < 3; ++k) pos4[(size_t)(4 * j + k)] = (float)pos[3 * j + k];
+    const size_t b_pos4 = pos4.size() * sizeof(float);
+    const size_t bytes = b_pos4 + nd * sizeof(double) + start.size() * sizeof(int32_t);
     FRT_HIP(hipMalloc(&G.map_mem[m], bytes));
-    FRT_HIP(hipMemcpy(G.map_mem[m], data.data(), nd * sizeof(double), hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy((char*)G.map_mem[m] + nd * sizeof(double), start.data(), start.size() * sizeof(int32_t),
+    char* mem = (char*)G.map_mem[m];
+    FRT_HIP(hipMemcpy(mem, pos4.data(), b_pos4, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4, data.data(), nd * sizeof(double), hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4 + nd * sizeof(double), start.data(), start.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
-    const double* base = (const double*)G.map_mem[m];
+    const double* base = (const double*)(mem + b_pos4);
+    M.pos4 = (const float*)mem;
     M.pos = base;
     M.power = base + 3 * std::max<int64_t>(n, 1);
     M.dir = base + 6 * std::max<int64_t>(n, 1);
-    M.start = (const int32_t*)((const char*)G.map_mem[m] + nd * sizeof(double));
+    M.start = (const int32_t*)(mem + b_pos4 + nd * sizeof(double));
     h->S.pmaps[m] = M;
     G.photons[m] = (uint64_t)n;
     return 0;

@@ -181,4 +181,201 @@ __device__ inline int64_t irradiance_estimate(const PhotonMapDev& M, const doubl
     return found;
 }
 
+// ---- wave-cooperative estimate ----
+// pm_irradiance_estimate with the 64 lanes of a wave working on ONE query
+// point (wave-uniform x): the neighbour cells' photons are scanned with
+// consecutive lanes on consecutive photons (coalesced binary32 positions),
+// those within the radius are compacted into the wave's LDS list, the k-th
+// smallest distance is found by a radix select over 24-bit keys of d^2 / r^2
+// (LDS histograms, at most three passes over the list), and the cone-filtered
+// sum is one more pass with a wave reduction. A list longer than kEstCap (a
+// dense caustic) is not stored: the select and sum passes then re-scan the
+// cells. Distances are binary32 here — the estimate is a statistical quantity
+// (the reference's photon maps come from drand48), the per-lane version
+// above keeps binary64.
+constexpr int kEstCap = 1024;
+
+struct EstLds {
+    float* d2;        // kEstCap: squared distances of the photons within the radius
+    int32_t* idx;     // kEstCap: their photon indices
+    unsigned* hist;   // 256
+};
+
+__device__ __forceinline__ int est_lane() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v) {
+    const int lane = est_lane();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ unsigned est_key(float d2, float inv_r2) {
+    const float q = d2 * inv_r2 * 16777216.0f;  // d^2 / r^2 as a 24-bit fixed-point key
+    return q >= 16777215.0f ? 16777215u : (unsigned)q;
+}
+
+// the neighbour cells (lane c < 27 owns cell c, dz outer, dx inner; each bucket once):
+// calls f(p, in, d2) for every chunk of up to 64 consecutive photons of a cell, in
+// uniform control flow; `in`: this lane's photon exists and lies within the radius
+template <typename F>
+__device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, float r2f, F&& f) {
+    const int lane = est_lane();
+    const int ci = lane < 27 ? lane : 0;
+    int64_t c[3];
+    for (int k = 0; k < 3; ++k) c[k] = (int64_t)floor((x[k] - M.origin[k]) / M.cell);
+    const uint32_t b = grid_bucket(c[0] + ci % 3 - 1, c[1] + (ci / 3) % 3 - 1, c[2] + ci / 9 - 1, M.num_buckets);
+    bool dup = false;
+    for (int j = 0; j < 26; ++j) {
+        const uint32_t bj = (uint32_t)__shfl((int)b, j, 64);
+        dup = dup || (j < ci && bj == b);
+    }
+    const bool keep = lane < 27 && !dup;
+    const int32_t s0 = keep ? M.start[b] : 0, e0 = keep ? M.start[b + 1] : 0;
+    const float xf[3] = {(float)x[0], (float)x[1], (float)x[2]};
+    for (int q = 0; q < 27; ++q) {
+        const int32_t s = __builtin_amdgcn_readlane(s0, q), e = __builtin_amdgcn_readlane(e0, q);
+        for (int32_t base = s; base < e; base += 64) {
+            const int32_t p = base + lane;
+            bool in = p < e;
+            float d2 = 0.0f;
+            if (in) {
+                const float4 pp = reinterpret_cast<const float4*>(M.pos4)[p];
+                const float dx = pp.x - xf[0], dy = pp.y - xf[1], dz = pp.z - xf[2];
+                d2 = dx * dx + dy * dy + dz * dz;
+                in = d2 < r2f;
+            }
+            f(p, in, d2);
+        }
+    }
+}
+
+// all 64 lanes call with the same x / normal; returns the photons used (the
+// reference's `found`) and the irradiance, in every lane
+__device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
+                                                   double max_dist, int k, double cone_k, double* irrad,
+                                                   const EstLds& L) {
+    irrad[0] = irrad[1] = irrad[2] = 0.0;
+    if (M.count <= 0) return 0;
+    const int lane = est_lane();
+    const double r2 = max_dist * max_dist;
+    const float r2f = (float)r2, inv_r2 = (float)(1.0 / r2);
+    // pass 1: the photons within the radius, compacted into the LDS list in scan order
+    unsigned total = 0;
+    wave_scan_cells(M, x, r2f, [&](int32_t p, bool in, float d2) {
+        const unsigned long long m = __ballot(in);
+        if (in) {
+            const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
+            if (at < (unsigned)kEstCap) {
+                L.d2[at] = d2;
+                L.idx[at] = p;
+            }
+        }
+        total += (unsigned)__popcll(m);
+    });
+    const unsigned found = total < (unsigned)k ? total : (unsigned)k;
+    if (found < 8) return found;
+    const bool listed = total <= (unsigned)kEstCap;
+    // every pass visits the in-range photons in the same order: from the list, or a re-scan
+    auto visit = [&](auto&& fn) {
+        if (listed) {
+            for (unsigned base = 0; base < total; base += 64) {
+                const unsigned i = base + (unsigned)lane;
+                const bool in = i < total;
+                fn(in ? L.idx[i] : 0, in, in ? L.d2[i] : 0.0f);
+            }
+        } else {
+            wave_scan_cells(M, x, r2f, fn);
+        }
+    };
+    // the k-th smallest key: radix select, 8 bits per pass
+    unsigned prefix = 0, mask = 0, need = found;
+    bool resolved = total <= (unsigned)k;  // every photon in range is used
+    for (int shift = 16; shift >= 0 && !resolved; shift -= 8) {
+        for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        visit([&](int32_t, bool in, float d2) {
+            const unsigned key = est_key(d2, inv_r2);
+            if (in && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
+        });
+        __builtin_amdgcn_wave_barrier();
+        unsigned h4[4], local = 0;
+        for (int j = 0; j < 4; ++j) {
+            h4[j] = L.hist[4 * lane + j];
+            local += h4[j];
+        }
+        const unsigned incl = wave_incl_scan(local);
+        const unsigned long long hit = __ballot(incl >= need);
+        const int owner = __builtin_ctzll(hit);
+        // the owner lane walks its four bins
+        unsigned below = incl - local;
+        int bin = 4 * lane + 3;
+        unsigned cnt = h4[3];
+        for (int j = 0; j < 4; ++j) {
+            if (below + h4[j] >= need) {
+                bin = 4 * lane + j;
+                cnt = h4[j];
+                break;
+            }
+            below += h4[j];
+        }
+        bin = __builtin_amdgcn_readlane(bin, owner);
+        cnt = __builtin_amdgcn_readlane(cnt, owner);
+        below = __builtin_amdgcn_readlane(below, owner);
+        need -= below;
+        prefix |= (unsigned)bin << shift;
+        mask |= 255u << shift;
+        resolved = cnt == need;
+    }
+    // sum pass (pm.c:125-145): keys below the k-th are in; at the k-th key the first `need` met
+    const double cone_r = cone_k * max_dist;
+    double acc[3] = {0.0, 0.0, 0.0};
+    float dmax = 0.0f;
+    unsigned ties = 0;
+    const bool all = total <= (unsigned)k;
+    visit([&](int32_t p, bool in, float d2) {
+        const unsigned key = est_key(d2, inv_r2);
+        const bool lower = in && (all || (key & mask) < prefix);
+        const bool tie = in && !all && (key & mask) == prefix;
+        const unsigned long long tm = __ballot(tie);
+        const bool take = lower || (tie && (resolved || ties + (unsigned)__popcll(tm & ((1ull << lane) - 1)) < need));
+        ties += (unsigned)__popcll(tm);
+        if (take) {
+            dmax = fmaxf(dmax, d2);
+            const double weight = 1.0 - sqrt((double)d2) / cone_r;
+            const double* dd = M.dir + 3 * (int64_t)p;
+            if ((dd[0] * normal[0] + dd[1] * normal[1] + dd[2] * normal[2]) < 0.0) {
+                const double* w3 = M.power + 3 * (int64_t)p;
+                acc[0] += w3[0] * weight;
+                acc[1] += w3[1] * weight;
+                acc[2] += w3[2] * weight;
+            }
+        }
+    });
+    for (int j = 0; j < 3; ++j) irrad[j] = wave_sum_d(acc[j]);
+    dmax = wave_max_f(dmax);
+    // np.dist2[0]: max_dist^2 until the heap filled, then its largest entry (pm.c:244)
+    const double d0 = all ? r2 : (double)dmax;
+    const double tmp = 1.0 / ((1.0 - 2.0 / (3.0 * cone_k)) * (kPi * d0));
+    irrad[0] *= tmp;
+    irrad[1] *= tmp;
+    irrad[2] *= tmp;
+    return found;
+}
+
 }  // namespace frt

@@ -70,6 +70,7 @@ __device__ __forceinline__ void frame_cache(const Ray& r, FrameCache& c) {
 
 // one photon map (frt_gi.hpp): photons sorted by grid bucket (SoA), built on the host after tracing
 struct PhotonMapDev {
+    const float* pos4;    // 4 per photon: binary32 x, y, z, 0 (the estimate's candidate scan)
     const double* pos;    // 3 per photon
     const double* power;  // 3 per photon (scaled by 1 / photon_count)
     const double* dir;    // 3 per photon: pm_photon_dir of the stored theta / phi bytes (pm.c:80-88)
