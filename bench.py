@@ -38,7 +38,10 @@ ASSETS = os.path.join(GOLDEN, "assets")
 DEFAULT_SCENE = "cornell_direct_800_4x4"
 CPU_SAMPLE_SCENE = "cornell_direct_200_4x4_t16"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_TRAFFIC_FILE = "r01_pmc_traffic.json"  # FETCH_SIZE + MemWrites32B of k_shadow, per launch
+PMC_FILE = "r01_pmc_shadow.json"  # tools/profile_round.sh + profile_summary.py: FETCH/WRITE_SIZE, SQ_* of the shadow kernel
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 binary64 VALU instruction per SIMD per ~4 cycles
+# (profiles/r01_microbench_valu.txt: v_fma/add/mul_f64 4.6-5.0 cycles per wave-op) at the 2.4 GHz peak clock
+VALU_PEAK_GINST_S = 1024 * 2.4 / 4.0
 
 # algorithmic HBM bytes of k_shadow ("byte model"), reported by the engine per frame as
 # stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point,
@@ -166,19 +169,27 @@ def main():
         avg_ms = kernel_ms[dom] / max(1, launches[dom])
         roof = None
         if dom == "shadow":
+            kname = "frt_jit_shadow" if last.get("shadow_jit") else "k_shadow"
             bytes_per_frame = last["shadow_kernel_bytes"]  # engine-side byte model (see above)
             per_launch = bytes_per_frame / max(1, launches[dom] / args.steps)
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": "k_shadow",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kname,
                     "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": round(per_launch)}
-            # HBM bytes per launch from the committed PMC passes of this kernel (tools/profile_round.sh)
-            pmc = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
+            # HBM bytes and VALU instructions per launch from the committed PMC passes of this kernel
+            # on this workload (tools/profile_round.sh); the kernel is VALU-issue bound, not HBM bound:
+            # "valu" relates its instruction count to the live kernel time
+            pmc = os.path.join(ROOT, "profiles", PMC_FILE)
             if os.path.exists(pmc):
                 t = json.load(open(pmc))
-                if t.get("kernel") == "k_shadow" and t.get("workload") == args.scene:
+                if t.get("kernel") == kname and t.get("workload") == args.scene:
                     roof["traffic"] = round(t["traffic_bytes_per_launch"])
-                    roof["traffic_source"] = "profiles/" + PMC_TRAFFIC_FILE
+                    roof["traffic_source"] = "profiles/" + PMC_FILE
+                    if "SQ_INSTS_VALU_per_launch" in t:
+                        ginst = t["SQ_INSTS_VALU_per_launch"] / (avg_ms * 1e-3) / 1e9
+                        roof["valu"] = {"achieved": round(ginst, 1), "peak": VALU_PEAK_GINST_S,
+                                        "unit": "G wave64 VALU inst/s", "frac": round(ginst / VALU_PEAK_GINST_S, 3),
+                                        "valu_inst_per_64_rays": round(t.get("valu_insts_per_wave", 0), 1)}
         else:
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": dom, "avg_launch_ms": round(avg_ms, 4)}
