@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1171,6 +1172,7 @@ static void build_walk_nodes(const frt_scene* sc, std::vector<frt::WalkNode>& wn
         return true;
     };
     wn.assign((size_t)std::max(1, sc->num_nodes), frt::WalkNode{});
+    std::vector<std::array<double, 12>> comp((size_t)std::max(1, sc->num_nodes));
     for (int i = 0; i < sc->num_nodes; ++i) {
         const frt_node& nd = sc->nodes[i];
         frt::WalkNode& w = wn[(size_t)i];
@@ -1192,6 +1194,33 @@ static void build_walk_nodes(const frt_scene* sc, std::vector<frt::WalkNode>& wn
         const double* mi = nd.xform >= 0 ? sc->xforms + 16 * (size_t)nd.xform : nullptr;
         if (mi)
             for (int k = 0; k < 12; ++k) w.m[k] = mi[k];
+        // composed world -> node map: C = M_node * C_parent (pre-order: the parent is done)
+        w.parent = nd.parent;
+        {
+            double cp[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+            if (nd.parent >= 0) std::memcpy(cp, comp[(size_t)nd.parent].data(), sizeof(cp));
+            double c[12];
+            if (mi) {
+                for (int r = 0; r < 3; ++r) {
+                    for (int q = 0; q < 4; ++q) {
+                        double v = 0.0;
+                        for (int j = 0; j < 3; ++j) v += mi[4 * r + j] * cp[4 * j + q];
+                        c[4 * r + q] = q == 3 ? v + mi[4 * r + 3] : v;
+                    }
+                }
+            } else {
+                std::memcpy(c, cp, sizeof(c));
+            }
+            std::memcpy(comp[(size_t)i].data(), c, sizeof(c));
+            double n1 = 0.0, tt = 0.0;
+            for (int r = 0; r < 3; ++r) {
+                n1 = std::max(n1, std::fabs(c[4 * r]) + std::fabs(c[4 * r + 1]) + std::fabs(c[4 * r + 2]));
+                tt = std::max(tt, std::fabs(c[4 * r + 3]));
+                for (int q = 0; q < 4; ++q) w.cm[4 * r + q] = (float)c[4 * r + q];
+            }
+            w.cN = std::nextafter((float)(n1 * (1.0 + 1e-9)), INFINITY);
+            w.cT = std::nextafter((float)(tt * (1.0 + 1e-9)), INFINITY);
+        }
         for (int r = 0; r < 3; ++r) {
             w.mrow_l1[r] = 0.f;
             for (int c = 0; c < 3; ++c) {

@@ -91,5 +91,148 @@ __device__ __forceinline__ bool finite_ray(const Ray& r, double dist) {
     return f;
 }
 
+// ---- binary32 interval walk ----
+// The walk above takes the reference's binary64 arithmetic step for step. Its
+// decisions (box hit, entries, t <= 0, t < distance, the order of two entries)
+// can mostly be proven from binary32 values with an error bound: every t is
+// carried as an interval [lo, hi] that contains the reference's binary64 value,
+// and a decision is taken only when the intervals settle it. A lane meeting an
+// undecidable comparison (or a direction component near the reference's
+// EPSILON slab branch) is marked `amb` and re-walked with the binary64 code.
+//
+// Error model (u = 2^-24, round to nearest; v_rcp_f32 within 1 ulp = 2u):
+//  * frame: node k's ray = C_k (world ray), C_k = M_k ... M_1 composed in binary64 at upload,
+//    evaluated as a 3-term fma chain on binary32 operands. Against the reference's sequential
+//    binary64 transforms: |o - o_ref|_inf <= eo = 6u (cN |o_w|_inf + cT), |d - d_ref|_inf <= ed
+//    = 6u cN (|d_w|_inf <= 1, normalised) — 3u for the chain, u for each of the world-ray and
+//    matrix roundings, the reference's own rounding (~1e-16) and the bound's rounding in the rest.
+//  * slab value t = (b - o_a) / d_a: |t~ - t_ref| <= 4.2u |t~| + (eo + u |b|) / |d_ref| + |t~| ed / |d_ref|
+//    with 1 / |d_ref| <= 1 / (|d~_a| - ed); taken as 7u |t~| + ... and x1.01 on the
+//    rest, covering the roundings of the bound arithmetic and of the interval ends.
+//  * tmin = max of the axes' low values, tmax = min of the high ones: intervals of a max / min
+//    are the max / min of the intervals.
+constexpr float kU = 0x1p-24f;
+constexpr float kXfErr = 6.0f * kU;
+constexpr float kSlabRel = 7.0f * kU;
+constexpr float kSlack = 1.01f;
+
+struct Iv {
+    float lo, hi;
+};
+
+// tri-state comparisons on intervals: 1 true, 0 false, -1 undecided
+__device__ __forceinline__ int iv_le(const Iv& a, const Iv& b) { return a.hi <= b.lo ? 1 : (a.lo > b.hi ? 0 : -1); }
+__device__ __forceinline__ int iv_le0(const Iv& a) { return a.hi <= 0.0f ? 1 : (a.lo > 0.0f ? 0 : -1); }
+__device__ __forceinline__ int iv_lt(const Iv& a, const Iv& b) { return a.hi < b.lo ? 1 : (a.lo >= b.hi ? 0 : -1); }
+
+__device__ __forceinline__ Iv iv_of(double x) { return Iv{__double2float_rd(x), __double2float_ru(x)}; }
+
+struct World32 {
+    float o[3], d[3], omax;
+};
+
+__device__ __forceinline__ void world32(const Ray& r, World32& w) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w.o[a] = (float)r.o[a];
+        w.d[a] = (float)r.d[a];
+    }
+    w.omax = fmaxf(fmaxf(fabsf(w.o[0]), fabsf(w.o[1])), fabsf(w.o[2]));
+}
+
+struct F32 {
+    float o[3], d[3], eo, ed;
+};
+
+__device__ __forceinline__ void frame32i(const WalkNode& nd, const World32& w, F32& f) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float* c = nd.cm + 4 * r;
+        f.o[r] = fmaf(c[0], w.o[0], fmaf(c[1], w.o[1], fmaf(c[2], w.o[2], c[3])));
+        f.d[r] = fmaf(c[0], w.d[0], fmaf(c[1], w.d[1], c[2] * w.d[2]));
+    }
+    f.eo = kXfErr * fmaf(nd.cN, w.omax, nd.cT);
+    f.ed = kXfErr * nd.cN;
+}
+
+// the slab entries tmin / tmax as intervals; false when |d_a| may be below EPSILON
+__device__ __forceinline__ bool slab_iv(const F32& f, const float* lo, const float* hi, float bmax, Iv& tmin,
+                                        Iv& tmax) {
+    bool ok = true;
+    float Ll = -__builtin_inff(), Lh = -__builtin_inff(), Hl = __builtin_inff(), Hh = __builtin_inff();
+    const float ab = (f.eo + bmax * kU) * kSlack;
+    const float eds = f.ed * kSlack;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float ad = fabsf(f.d[a]) - f.ed;
+        ok = ok && ad >= kEps32;
+        const float ir = __builtin_amdgcn_rcpf(ad);
+        const float r = __builtin_amdgcn_rcpf(f.d[a]);
+        const float k1 = fmaf(eds, ir, kSlabRel), k0 = ab * ir;
+        const float t0 = (lo[a] - f.o[a]) * r, t1 = (hi[a] - f.o[a]) * r;
+        const float e = fmaf(fmaxf(fabsf(t0), fabsf(t1)), k1, k0);
+        const float mn = fminf(t0, t1), mx = fmaxf(t0, t1);
+        Ll = fmaxf(Ll, mn - e);
+        Lh = fmaxf(Lh, mn + e);
+        Hl = fminf(Hl, mx - e);
+        Hh = fminf(Hh, mx + e);
+    }
+    tmin = Iv{Ll, Lh};
+    tmax = Iv{Hl, Hh};
+    return ok;
+}
+
+// a composite's box (bounding_box.c:164-175) in its own frame: 1 enter, 0 skip, -1 undecided
+__device__ __forceinline__ int box_enter32(const WalkNode& nd, const F32& f, bool skip_behind) {
+    Iv tmin, tmax;
+    const float bmax = fmaxf(fmaxf(nd.bmag[0], nd.bmag[1]), nd.bmag[2]);
+    if (!slab_iv(f, nd.bb32, nd.bb32 + 3, bmax, tmin, tmax)) return -1;
+    const int hit = iv_le(tmin, tmax);
+    if (hit <= 0) return hit;
+    if (skip_behind && behind((double)tmax.hi)) return 0;  // wholly behind the ray (an upper bound is behind)
+    return 1;
+}
+
+// unit cube entries (cube.c:56-77): ex = 1 two entries, 0 none, -1 undecided
+__device__ __forceinline__ int cube_iv(const WalkNode& nd, const World32& w, Iv& t0, Iv& t1) {
+    F32 f;
+    frame32i(nd, w, f);
+    const float lo[3] = {-1.0f, -1.0f, -1.0f}, hi[3] = {1.0f, 1.0f, 1.0f};
+    if (!slab_iv(f, lo, hi, 1.0f, t0, t1)) return -1;
+    return iv_le(t0, t1);
+}
+
+// a cube outside CSG units: leaf_top's decisions on intervals; undecided -> amb
+__device__ __forceinline__ void cube_top32(const WalkNode& nd, const World32& w, const Iv& dist, bool act, bool& alive,
+                                           int& result, bool& any_entry, bool& amb) {
+    Iv ta, tb;
+    const int ex = cube_iv(nd, w, ta, tb);
+    if (!act) return;
+    const int za = iv_le0(ta), zb = iv_le0(tb);
+    const int la = iv_lt(ta, dist), lb = iv_lt(tb, dist);
+    if (ex < 0 || (ex > 0 && (za < 0 || zb < 0 || (za == 0 && la < 0) || (zb == 0 && lb < 0)))) {
+        amb = true;
+        alive = false;
+        return;
+    }
+    if (ex == 0) return;
+    any_entry = true;
+    if (za == 0 || zb == 0) {  // an entry that is not <= 0 ends the walk
+        const bool blocked = (za == 0 && la == 1) || (zb == 0 && lb == 1);
+        result = blocked && nd.casts ? 1 : 0;
+        alive = false;
+    }
+}
+
+// sorted entries of a non-cube leaf inside a CSG unit, exactly (binary64 ray of its parent frame)
+template <int kType, bool kXf>
+__device__ __forceinline__ void leaf_slots_iv(const DevScene& S, const WalkNode& nd, const Ray& R, bool act, Iv& t0,
+                                              Iv& t1, bool& v0, bool& v1) {
+    double a, b;
+    leaf_slots<kType, kXf>(S, nd, R, act, a, b, v0, v1);
+    t0 = iv_of(a);
+    t1 = iv_of(b);
+}
+
 }  // namespace jit
 }  // namespace frt

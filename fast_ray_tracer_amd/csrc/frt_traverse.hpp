@@ -48,7 +48,14 @@ struct alignas(16) WalkNode {
     float mrow_l1[3];                  // their L1 norms
     float bb32[6];                     // composites: f32(bbox) (box32)
     float bmag[3];                     // composites: max(|lo_a|, |hi_a|) rounded up (box32's error bound)
-    int32_t pad32;
+    int32_t parent;                    // parent node (-1: a world shape)
+    // world -> this node's frame as one affine map (the product of the inverse transforms from the
+    // world shape down to this node, composed in binary64 at upload), rounded to binary32, with the
+    // bounds frt_jit_rt.hpp's interval walk needs: cN = max row L1 norm of the 3x3 part, cT = max
+    // |translation|, both rounded up
+    float cm[12];
+    float cN, cT;
+    int32_t pad2[2];
 };
 
 // per-frame cache of the current ray: reciprocal direction (two Newton steps),
