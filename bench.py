@@ -39,9 +39,9 @@ DEFAULT_SCENE = "cornell_direct_800_4x4"
 CPU_SAMPLE_SCENE = "cornell_direct_200_4x4_t16"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 PMC_FILE = "r01_pmc_shadow.json"  # tools/profile_round.sh + profile_summary.py: FETCH/WRITE_SIZE, SQ_* of the shadow kernel
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 binary64 VALU instruction per SIMD per ~4 cycles
-# (profiles/r01_microbench_valu.txt: v_fma/add/mul_f64 4.6-5.0 cycles per wave-op) at the 2.4 GHz peak clock
-VALU_PEAK_GINST_S = 1024 * 2.4 / 4.0
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 2 cycles (SIMD32; binary64
+# and transcendental instructions take 2-4x: profiles/r01_microbench_valu.txt) at the 2.4 GHz peak clock
+VALU_PEAK_GINST_S = 1024 * 2.4 / 2.0
 
 # algorithmic HBM bytes of k_shadow ("byte model"), reported by the engine per frame as
 # stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point,
