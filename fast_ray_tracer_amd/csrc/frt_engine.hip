@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<Node
                                 double ndh = fmax(0.0, dot3(nr.normalv, hv));
                                 double edh_inv = 1.0 / fmax(0.0, dot3(nr.eyev, hv));
                                 double ldh = dot3(lv, hv);
-                                double dist_term = (nr.Ns + 2) * pow(ndh, nr.Ns) * 0.5 * k1Pi;
+                                double dist_term = (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
                                 double gc = 2.0 * ndh * edh_inv;
                                 double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
                                 // pow(1 - ldh, 5.0) (renderer.c:969) by squaring: within an ulp or two of the
@@ -917,7 +917,7 @@ __global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed
 // color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray, scaled by the sample's
 // first coordinate (final_gather: "scale by theta"); the photon estimates wave-cooperatively
 template <bool kPat>
-__global__ void __launch_bounds__(kBlock) k_gather_shade(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) k_gather_shade(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
                                                          const HitRec* __restrict__ hits, int64_t n,
                                                          double* __restrict__ gather_col) {
     FRT_EST_LDS(lds);

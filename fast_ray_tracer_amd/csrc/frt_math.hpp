@@ -178,6 +178,26 @@ __device__ __forceinline__ bool box_decide(const double* bb, const Ray& r, const
     return box_range(bb, r, a, b);
 }
 
+// pow(x, y) of the microfacet distribution term (renderer.c:966): an integral
+// exponent (the usual Ns) by binary exponentiation — a few ulps from the
+// reference's libm pow, like the device pow it replaces, at a fraction of its
+// cost; other exponents through pow
+__device__ __attribute__((noinline)) double pow_general(double x, double y) { return pow(x, y); }
+
+__device__ __forceinline__ double pow_ns(double x, double y) {
+    if (y >= 0.0 && y < 4096.0 && y == __builtin_floor(y)) {
+        const unsigned e = (unsigned)y;
+        double r = 1.0, b = x;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {  // fixed trip count: no loop-carried divergence
+            r = (e >> k) & 1u ? r * b : r;
+            b *= b;
+        }
+        return r;
+    }
+    return pow_general(x, y);
+}
+
 // ---- wave-aggregated counters ----
 // One atomic per wave instead of one per lane: a single shared counter taking
 // an atomic from every path node serialises at its L2 channel (the queue
