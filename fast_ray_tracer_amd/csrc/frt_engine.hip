@@ -1040,6 +1040,7 @@ struct frt_scene_handle {
     int64_t* redo = nullptr;           // lanes handed back to the generic walk
     unsigned* redo_count = nullptr;
     unsigned redo_cap = 0;
+    unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks
     // work buffers (grow on demand)
     struct Level {
         frt::Cols<frt::NodeRec> rec;
@@ -1358,6 +1359,14 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                 h->owned.push_back(p);
                 h->redo = (int64_t*)p;
                 h->redo_count = (unsigned*)(h->redo + h->redo_cap);
+                if (std::getenv("FRT_JIT_STATS")) {
+                    if (hipMalloc((void**)&h->jit_stats, 64 * 32 * sizeof(unsigned long long)) != hipSuccess) {
+                        frt_scene_release(h);
+                        return fail("frt_scene_upload: jit stats allocation failed");
+                    }
+                    h->owned.push_back(h->jit_stats);
+                    hip_ignore(hipMemset(h->jit_stats, 0, 64 * 32 * sizeof(unsigned long long)));
+                }
             } else if (std::getenv("FRT_JIT_VERBOSE")) {
                 std::fprintf(stderr, "frt: generic shadow walk (%s)\n", why.c_str());
             }
@@ -1449,6 +1458,18 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
 void frt_scene_release(frt_scene_handle* h) {
     if (!h) return;
     hip_ignore(hipSetDevice(h->device));
+    if (h->jit_stats) {
+        std::vector<unsigned long long> c(64 * 32);
+        if (hipMemcpy(c.data(), h->jit_stats, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
+            unsigned long long live = 0, amb = 0;
+            for (int j = 0; j < 64; ++j) {
+                live += c[32 * j];
+                amb += c[32 * j + 1];
+            }
+            std::fprintf(stderr, "frt jit stats: live shadow lanes %llu, re-walked in binary64 %llu (%.4f%%)\n", live, amb,
+                         live ? 100.0 * (double)amb / (double)live : 0.0);
+        }
+    }
     for (void* p : h->owned) hip_ignore(hipFree(p));
     for (auto& L : h->levels) {
         hip_ignore(hipFree(L.rec.w));
@@ -1601,7 +1622,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         int64_t work = n * h->samples_per_node;
         hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
         void* args[] = {&h->S, (void*)&B, (void*)&rec, &n, &h->j_light, &h->j_point, &h->samples_per_node,
-                        &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err};
+                        &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
         hip_ignore(hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(work, frt::kTraceBlock), 1, 1,
                                          frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr));
         switch (h->S.features & 3) {
