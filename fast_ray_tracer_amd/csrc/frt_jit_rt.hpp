@@ -159,9 +159,9 @@ __device__ __forceinline__ void frame32i(const WalkNode& nd, const World32& w, F
 __device__ __forceinline__ bool slab_iv(const F32& f, const float* lo, const float* hi, float bmax, Iv& tmin,
                                         Iv& tmax) {
     bool ok = true;
-    float Ll = -__builtin_inff(), Lh = -__builtin_inff(), Hl = __builtin_inff(), Hh = __builtin_inff();
     const float ab = (f.eo + bmax * kU) * kSlack;
     const float eds = f.ed * kSlack;
+    float Ll = 0.0f, Lh = 0.0f, Hl = 0.0f, Hh = 0.0f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float ad = fabsf(f.d[a]) - f.ed;
@@ -172,10 +172,17 @@ __device__ __forceinline__ bool slab_iv(const F32& f, const float* lo, const flo
         const float t0 = (lo[a] - f.o[a]) * r, t1 = (hi[a] - f.o[a]) * r;
         const float e = fmaf(fmaxf(fabsf(t0), fabsf(t1)), k1, k0);
         const float mn = fminf(t0, t1), mx = fmaxf(t0, t1);
-        Ll = fmaxf(Ll, mn - e);
-        Lh = fmaxf(Lh, mn + e);
-        Hl = fminf(Hl, mx - e);
-        Hh = fminf(Hh, mx + e);
+        if (a == 0) {  // (the first axis starts the max / min chains)
+            Ll = mn - e;
+            Lh = mn + e;
+            Hl = mx - e;
+            Hh = mx + e;
+        } else {
+            Ll = fmaxf(Ll, mn - e);
+            Lh = fmaxf(Lh, mn + e);
+            Hl = fminf(Hl, mx - e);
+            Hh = fminf(Hh, mx + e);
+        }
     }
     tmin = Iv{Ll, Lh};
     tmax = Iv{Hl, Hh};
@@ -189,7 +196,8 @@ __device__ __forceinline__ int box_enter32(const WalkNode& nd, const F32& f, boo
     if (!slab_iv(f, nd.bb32, nd.bb32 + 3, bmax, tmin, tmax)) return -1;
     const int hit = iv_le(tmin, tmax);
     if (hit <= 0) return hit;
-    if (skip_behind && behind((double)tmax.hi)) return 0;  // wholly behind the ray (an upper bound is behind)
+    // wholly behind the ray: an upper bound of tmax is behind (walk()'s behind(), in binary32)
+    if (skip_behind && tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi))) return 0;
     return 1;
 }
 
