@@ -839,7 +839,8 @@ __device__ inline void wave_photon_estimates(const PhotonMapDev& M, const DevSce
         }
         // the reference passes eyev as the estimate's normal (renderer.c:875)
         const int64_t used = wave_irradiance_estimate(M, x, nrm, S.cfg.irradiance_radius, S.cfg.irradiance_num,
-                                                      S.cfg.cone_filter_k, e, L);
+                                                      S.cfg.cone_filter_k, e, L,
+                                                      S.dbg ? S.dbg + kDbgProf + 13 : nullptr);
         if (est_lane() == j && used > 0) {
             const double f = scale_num / (double)used;
             for (int k = 0; k < 3; ++k) est[k] = e[k] * f;
@@ -1900,6 +1901,8 @@ static void dump_walk_stats(frt_scene_handle* h) {
     std::fprintf(stderr, "walk prof (shadow, cycles):");
     const char* pn[8] = {"setup", "close", "xf_pop", "composite", "leaf_xf", "leaf_test", "leaf_post", "loop"};
     for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s=%llu", pn[k], c[frt::kDbgProf + k]);
+    std::fprintf(stderr, "\nestimate prof (cycles): scan=%llu select=%llu sum=%llu", c[frt::kDbgProf + 13],
+                 c[frt::kDbgProf + 14], c[frt::kDbgProf + 15]);
     std::fprintf(stderr, "\nprepare prof (cycles):");
     const char* qn[5] = {"ray", "hits_load", "prepare", "spawn", "stores"};
     for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s=%llu", qn[k], c[frt::kDbgProf + 8 + k]);

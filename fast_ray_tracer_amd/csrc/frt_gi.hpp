@@ -267,11 +267,24 @@ __device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, f
 
 // all 64 lanes call with the same x / normal; returns the photons used (the
 // reference's `found`) and the irradiance, in every lane
+#ifdef FRT_WALK_PROF
+#define EST_STAMP(k)                                                                      \
+    do {                                                                                  \
+        const unsigned long long t1_ = prof_stamp();                                      \
+        if (lane == 0 && prof) atomicAdd(prof + (k), t1_ - est_t0);                      \
+        est_t0 = t1_;                                                                     \
+    } while (0)
+#else
+#define EST_STAMP(k)
+#endif
 __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
                                                    double max_dist, int k, double cone_k, double* irrad,
-                                                   const EstLds& L) {
+                                                   const EstLds& L, unsigned long long* prof = nullptr) {
     irrad[0] = irrad[1] = irrad[2] = 0.0;
     if (M.count <= 0) return 0;
+#ifdef FRT_WALK_PROF
+    unsigned long long est_t0 = prof_stamp();
+#endif
     const int lane = est_lane();
     const double r2 = max_dist * max_dist;
     const float r2f = (float)r2, inv_r2 = (float)(1.0 / r2);
@@ -288,6 +301,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         }
         total += (unsigned)__popcll(m);
     });
+    EST_STAMP(0);
     const unsigned found = total < (unsigned)k ? total : (unsigned)k;
     if (found < 8) return found;
     const bool listed = total <= (unsigned)kEstCap;
@@ -342,6 +356,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         mask |= 255u << shift;
         resolved = cnt == need;
     }
+    EST_STAMP(1);
     // sum pass (pm.c:125-145): keys below the k-th are in; at the k-th key the first `need` met
     const double cone_r = cone_k * max_dist;
     double acc[3] = {0.0, 0.0, 0.0};
@@ -369,6 +384,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     });
     for (int j = 0; j < 3; ++j) irrad[j] = wave_sum_d(acc[j]);
     dmax = wave_max_f(dmax);
+    EST_STAMP(2);
     // np.dist2[0]: max_dist^2 until the heap filled, then its largest entry (pm.c:244)
     const double d0 = all ? r2 : (double)dmax;
     const double tmp = 1.0 / ((1.0 - 2.0 / (3.0 * cone_k)) * (kPi * d0));
