@@ -805,17 +805,6 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
     for (int k = 0; k < 3; ++k) next_power[3 * at + k] = np[k];
 }
 
-// lighting_gi (renderer.c:863-892) / lighting_caustics (renderer.c:829-861) estimate at a surface point
-__device__ inline void photon_estimate(const PhotonMapDev& M, const DevScene& S, const double* point,
-                                       const double* eyev, double scale_num, double* est) {
-    const int64_t used = irradiance_estimate(M, point, eyev /* the reference passes eyev as the normal */,
-                                             S.cfg.irradiance_radius, S.cfg.irradiance_num, S.cfg.cone_filter_k, est);
-    if (used > 0) {
-        const double f = scale_num / (double)used;
-        for (int k = 0; k < 3; ++k) est[k] *= f;
-    }
-}
-
 // the wave's LDS for wave_irradiance_estimate (frt_gi.hpp); blocks of kBlock threads
 #define FRT_EST_LDS(name)                                                    \
     __shared__ float name##_d2[kBlock / 64][kEstCap];                        \
@@ -1748,72 +1737,86 @@ static void quantized_dir(const double* d, double* out) {
     out[2] = std::cos(ta);
 }
 
-// hashed uniform grid over the photons (frt_gi.hpp for_photons_within): one
-// allocation per map, photons sorted by bucket
+// dense uniform grid over the photons (frt_gi.hpp wave_scan_cells): cell edge
+// radius / 3, doubled while the grid would exceed kMaxGridCells; photons sorted
+// by cell, x fastest (a row of cells is one contiguous range); one allocation
+// per map: binary32 positions | power + direction records | cell starts
+constexpr double kMaxGridCells = (double)(1 << 24);
+
 static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::StoredPhoton>& ph, double scale) {
     auto& G = h->gi;
     hip_ignore(hipFree(G.map_mem[m]));
     G.map_mem[m] = nullptr;
     frt::PhotonMapDev M{};
     const int64_t n = (int64_t)ph.size();
+    if (n > ((int64_t)1 << 30)) return fail("photon map too large");
     M.count = n;
-    M.cell = h->S.cfg.irradiance_radius > 0 ? h->S.cfg.irradiance_radius : 1.0;
-    int64_t nb = 1;
-    while (nb < 2 * n) nb <<= 1;
-    if (nb > ((int64_t)1 << 30) || n > ((int64_t)1 << 30)) return fail("photon map too large");
-    M.num_buckets = (int32_t)nb;
-    for (int k = 0; k < 3; ++k) M.origin[k] = 0.0;
-    if (n > 0)
+    double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};
+    bool first = true;
+    for (const auto& p : ph) {
+        if (!(std::isfinite(p.pos[0]) && std::isfinite(p.pos[1]) && std::isfinite(p.pos[2]))) continue;
         for (int k = 0; k < 3; ++k) {
-            double lo = ph[0].pos[k];
-            for (const auto& p : ph) lo = std::min(lo, p.pos[k]);
-            M.origin[k] = std::isfinite(lo) ? lo : 0.0;
+            lo[k] = first ? p.pos[k] : std::min(lo[k], p.pos[k]);
+            hi[k] = first ? p.pos[k] : std::max(hi[k], p.pos[k]);
         }
-    std::vector<uint32_t> bucket((size_t)n);
-    std::vector<int32_t> start((size_t)nb + 1, 0);
+        first = false;
+    }
+    double cell = (h->S.cfg.irradiance_radius > 0 ? h->S.cfg.irradiance_radius : 1.0) / 3.0;
+    int64_t dims[3];
+    for (;;) {
+        double cells = 1.0;
+        for (int k = 0; k < 3; ++k) {
+            const double d = std::floor((hi[k] - lo[k]) / cell) + 1.0;
+            dims[k] = d < 1e9 ? (int64_t)d : (int64_t)1e9;
+            cells *= (double)dims[k];
+        }
+        if (cells <= kMaxGridCells) break;
+        cell *= 2.0;
+    }
+    for (int k = 0; k < 3; ++k) {
+        M.origin[k] = lo[k];
+        M.dims[k] = (int32_t)dims[k];
+    }
+    M.cell = cell;
+    M.inv_cell = 1.0 / cell;
+    const int64_t ncells = dims[0] * dims[1] * dims[2];
+    // the cell of each photon, as the device computes it (floor((x - origin) * inv_cell)), clamped
+    std::vector<int32_t> cell_of((size_t)n), start((size_t)ncells + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
         int64_t c[3];
-        for (int k = 0; k < 3; ++k) c[k] = (int64_t)std::floor((ph[(size_t)i].pos[k] - M.origin[k]) / M.cell);
-        const uint64_t hsh = (uint64_t)c[0] * 73856093ull ^ (uint64_t)c[1] * 19349663ull ^ (uint64_t)c[2] * 83492791ull;
-        bucket[(size_t)i] = (uint32_t)(host_mix64(hsh) & (uint64_t)(nb - 1));
-        start[bucket[(size_t)i] + 1]++;
+        for (int k = 0; k < 3; ++k) {
+            const double f = std::floor((ph[(size_t)i].pos[k] - M.origin[k]) * M.inv_cell);
+            c[k] = std::isfinite(f) ? (int64_t)std::min(std::max(f, 0.0), (double)(dims[k] - 1)) : 0;
+        }
+        cell_of[(size_t)i] = (int32_t)((c[2] * dims[1] + c[1]) * dims[0] + c[0]);
+        start[(size_t)cell_of[(size_t)i] + 1]++;
     }
-    for (int64_t b = 0; b < nb; ++b) start[(size_t)b + 1] += start[(size_t)b];
+    for (int64_t b = 0; b < ncells; ++b) start[(size_t)b + 1] += start[(size_t)b];
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
-    const size_t nd = (size_t)std::max<int64_t>(n, 1) * 9;
-    std::vector<double> data(nd, 0.0);
-    double* pos = data.data();
-    double* pow = pos + 3 * std::max<int64_t>(n, 1);
-    double* dir = pow + 3 * std::max<int64_t>(n, 1);
+    const size_t np = (size_t)std::max<int64_t>(n, 1);
+    std::vector<float> pos4(np * 4, 0.0f);
+    std::vector<double> pwdir(np * 6, 0.0);
     for (int64_t i = 0; i < n; ++i) {
         const auto& p = ph[(size_t)i];
-        const int64_t j = fill[bucket[(size_t)i]]++;
+        const int64_t j = fill[(size_t)cell_of[(size_t)i]]++;
         double d[3];
         quantized_dir(p.dir, d);
         for (int k = 0; k < 3; ++k) {
-            pos[3 * j + k] = p.pos[k];
-            pow[3 * j + k] = p.power[k] * scale;  // pm_scale_photon_power
-            dir[3 * j + k] = d[k];
+            pos4[(size_t)(4 * j + k)] = (float)p.pos[k];
+            pwdir[(size_t)(6 * j + k)] = p.power[k] * scale;  // pm_scale_photon_power
+            pwdir[(size_t)(6 * j + 3 + k)] = d[k];
         }
     }
-    // binary32 positions (x, y, z, 0) for the estimate's candidate scan (frt_gi.hpp)
-    std::vector<float> pos4((size_t)std::max<int64_t>(n, 1) * 4, 0.0f);
-    for (int64_t j = 0; j < n; ++j)
-        for (int k = 0; k < 3; ++k) pos4[(size_t)(4 * j + k)] = (float)pos[3 * j + k];
-    const size_t b_pos4 = pos4.size() * sizeof(float);
-    const size_t bytes = b_pos4 + nd * sizeof(double) + start.size() * sizeof(int32_t);
+    const size_t b_pos4 = pos4.size() * sizeof(float), b_pw = pwdir.size() * sizeof(double);
+    const size_t bytes = b_pos4 + b_pw + start.size() * sizeof(int32_t);
     FRT_HIP(hipMalloc(&G.map_mem[m], bytes));
     char* mem = (char*)G.map_mem[m];
     FRT_HIP(hipMemcpy(mem, pos4.data(), b_pos4, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4, data.data(), nd * sizeof(double), hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4 + nd * sizeof(double), start.data(), start.size() * sizeof(int32_t),
-                      hipMemcpyHostToDevice));
-    const double* base = (const double*)(mem + b_pos4);
+    FRT_HIP(hipMemcpy(mem + b_pos4, pwdir.data(), b_pw, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4 + b_pw, start.data(), start.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     M.pos4 = (const float*)mem;
-    M.pos = base;
-    M.power = base + 3 * std::max<int64_t>(n, 1);
-    M.dir = base + 6 * std::max<int64_t>(n, 1);
-    M.start = (const int32_t*)(mem + b_pos4 + nd * sizeof(double));
+    M.pwdir = (const double*)(mem + b_pos4);
+    M.start = (const int32_t*)(mem + b_pos4 + b_pw);
     h->S.pmaps[m] = M;
     G.photons[m] = (uint64_t)n;
     return 0;

@@ -1,7 +1,7 @@
 // frt-mi355x global illumination on the device: photon emission and the
 // photon_hit decisions of the reference's photon tracer (photon_tracer.c),
-// the k-nearest-photon irradiance estimate (pm.c:91-250) over a hashed
-// uniform grid, and the hemisphere sampling shared with the final gather
+// the k-nearest-photon irradiance estimate (pm.c:91-250) over a dense uniform
+// grid, and the hemisphere sampling shared with the final gather
 // (sampler.c:24-114, renderer.c:648-687).
 //
 // The reference draws from drand48 / rand(); the device uses the
@@ -48,151 +48,24 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
     normalize3(t, out);
 }
 
-// ---- photon maps on the device ----
-
-__device__ __forceinline__ uint32_t grid_bucket(int64_t ix, int64_t iy, int64_t iz, int32_t nb) {
-    const uint64_t h = (uint64_t)ix * 73856093ull ^ (uint64_t)iy * 19349663ull ^ (uint64_t)iz * 83492791ull;
-    return (uint32_t)(mix64(h) & (uint64_t)(nb - 1));
-}
-
-// Visit every photon within distance^2 < r2 of x exactly once: the 27 cells
-// around x's cell (cell edge >= radius), each bucket once even when cells
-// collide in the hash. f(index, d2) is called per photon inside the sphere.
-template <typename F>
-__device__ inline void for_photons_within(const PhotonMapDev& M, const double* x, double r2, F&& f) {
-    int64_t c[3];
-    for (int k = 0; k < 3; ++k) c[k] = (int64_t)floor((x[k] - M.origin[k]) / M.cell);
-    uint32_t seen[27];
-    int nseen = 0;
-    for (int dz = -1; dz <= 1; ++dz)
-        for (int dy = -1; dy <= 1; ++dy)
-            for (int dx = -1; dx <= 1; ++dx) {
-                const uint32_t b = grid_bucket(c[0] + dx, c[1] + dy, c[2] + dz, M.num_buckets);
-                bool dup = false;
-                for (int q = 0; q < nseen; ++q) dup = dup || seen[q] == b;
-                if (dup) continue;
-                seen[nseen++] = b;
-                const int32_t e = M.start[b + 1];
-                for (int32_t p = M.start[b]; p < e; ++p) {
-                    const double* pp = M.pos + 3 * (int64_t)p;
-                    // pm_locate_photons' distance (pm.c:185-191)
-                    double d1 = pp[0] - x[0];
-                    double d2 = d1 * d1;
-                    d1 = pp[1] - x[1];
-                    d2 += d1 * d1;
-                    d1 = pp[2] - x[2];
-                    d2 += d1 * d1;
-                    if (d2 < r2) f(p, d2);
-                }
-            }
-}
-
-// pm_irradiance_estimate (pm.c:91-155): the k nearest photons within
-// max_dist (the reference's max-heap in pm_locate_photons keeps exactly the k
-// smallest squared distances), cone-filtered, photons arriving from the
-// "normal" side only. The k-th distance is found by histogram refinement over
-// [0, max_dist^2) (a few passes over the candidates, bounded registers), the
-// sum is taken in one more pass. Returns the number of photons used; irradiance
-// is zero when fewer than 8 were found, as in the reference.
-__device__ inline int64_t irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
-                                              double max_dist, int k, double cone_k, double* irrad) {
-    irrad[0] = irrad[1] = irrad[2] = 0.0;
-    if (M.count <= 0) return 0;
-    const double r2 = max_dist * max_dist;
-    constexpr int kBins = 16;
-    // pass 1: count and histogram over [0, r2)
-    int64_t total = 0;
-    int32_t hist[kBins];
-    for (int b = 0; b < kBins; ++b) hist[b] = 0;
-    double lo = 0.0, hi = r2;
-    for_photons_within(M, x, r2, [&](int32_t, double d2) {
-        ++total;
-        int b = (int)(d2 / r2 * kBins);
-        b = b < 0 ? 0 : (b >= kBins ? kBins - 1 : b);
-        ++hist[b];
-    });
-    int64_t found = total < (int64_t)k ? total : (int64_t)k;
-    if (found < 8) return found;
-    // select: photons with d2 < lo are all in; `need` more come from [lo, hi)
-    int64_t need = found;
-    bool all_in_range = total <= (int64_t)k;
-    for (int level = 0; level < 12 && !all_in_range; ++level) {
-        int64_t cum = 0;
-        int b = 0;
-        for (; b < kBins; ++b) {
-            if (cum + hist[b] >= need) break;
-            cum += hist[b];
-        }
-        const double w = (hi - lo) / kBins;
-        const double nlo = lo + w * b, nhi = (b == kBins - 1) ? hi : lo + w * (b + 1);
-        need -= cum;
-        lo = nlo;
-        hi = nhi;
-        if (hist[b] == need || !(hi > lo)) {
-            all_in_range = hist[b] == need;
-            break;
-        }
-        for (int q = 0; q < kBins; ++q) hist[q] = 0;
-        const double llo = lo, lhi = hi, lw = hi - lo;
-        for_photons_within(M, x, r2, [&](int32_t, double d2) {
-            if (d2 >= llo && d2 < lhi) {
-                int q = (int)((d2 - llo) / lw * kBins);
-                q = q < 0 ? 0 : (q >= kBins ? kBins - 1 : q);
-                ++hist[q];
-            }
-        });
-    }
-    // sum pass (pm.c:125-145); exact ties at the boundary: the first `need` met are taken
-    int64_t taken_in_range = 0;
-    double dmax = 0.0;
-    const double llo = total <= (int64_t)k ? r2 : lo;
-    const double lhi = total <= (int64_t)k ? r2 : hi;
-    const double cone_r = cone_k * max_dist;
-    const double* pw = M.power;
-    const double* pd = M.dir;
-    const double* ps = M.pos;
-    for_photons_within(M, x, r2, [&](int32_t p, double d2) {
-        bool take = d2 < llo;
-        if (!take && d2 >= llo && d2 < lhi && taken_in_range < need) {
-            take = true;
-            ++taken_in_range;
-        }
-        if (total <= (int64_t)k) take = true;
-        if (!take) return;
-        if (d2 > dmax) dmax = d2;
-        const double* pp = ps + 3 * (int64_t)p;
-        const double dp = sqrt((x[0] - pp[0]) * (x[0] - pp[0]) + (x[1] - pp[1]) * (x[1] - pp[1]) +
-                               (x[2] - pp[2]) * (x[2] - pp[2]));
-        const double weight = 1.0 - dp / cone_r;
-        const double* dd = pd + 3 * (int64_t)p;
-        if ((dd[0] * normal[0] + dd[1] * normal[1] + dd[2] * normal[2]) < 0.0) {
-            const double* w3 = pw + 3 * (int64_t)p;
-            irrad[0] += w3[0] * weight;
-            irrad[1] += w3[1] * weight;
-            irrad[2] += w3[2] * weight;
-        }
-    });
-    // np.dist2[0]: max_dist^2 until the heap filled, then its largest entry (pm.c:244)
-    const double d0 = total < (int64_t)k ? r2 : (total == (int64_t)k ? r2 : dmax);
-    const double tmp = 1.0 / ((1.0 - 2.0 / (3.0 * cone_k)) * (kPi * d0));
-    irrad[0] *= tmp;
-    irrad[1] *= tmp;
-    irrad[2] *= tmp;
-    return found;
-}
-
 // ---- wave-cooperative estimate ----
-// pm_irradiance_estimate with the 64 lanes of a wave working on ONE query
-// point (wave-uniform x): the neighbour cells' photons are scanned with
-// consecutive lanes on consecutive photons (coalesced binary32 positions),
-// those within the radius are compacted into the wave's LDS list, the k-th
-// smallest distance is found by a radix select over 24-bit keys of d^2 / r^2
-// (LDS histograms, at most three passes over the list), and the cone-filtered
-// sum is one more pass with a wave reduction. A list longer than kEstCap (a
-// dense caustic) is not stored: the select and sum passes then re-scan the
-// cells. Distances are binary32 here — the estimate is a statistical quantity
-// (the reference's photon maps come from drand48), the per-lane version
-// above keeps binary64.
+// pm_irradiance_estimate (pm.c:91-155) with the 64 lanes of a wave working on
+// ONE query point (wave-uniform x): the k nearest photons within max_dist (the
+// reference's max-heap in pm_locate_photons keeps exactly the k smallest
+// squared distances), cone-filtered, photons arriving from the "normal" side
+// only; zero below 8 photons, as in the reference.
+//
+// Candidates come from the dense grid of PhotonMapDev (cell edge radius / 3):
+// the grid rows (y, z) within reach of the sphere, each clipped in x to the
+// sphere's chord, are concatenated and scanned 64 photons at a time
+// (coalesced binary32 positions); photons within the radius are compacted into
+// the wave's LDS list (ballot + rank), the k-th smallest distance is found by a
+// radix select over 24-bit keys of d^2 / r^2 (LDS histograms, at most three
+// passes over the list), and the cone-filtered sum is one more pass with a wave
+// reduction. A list longer than kEstCap (a dense caustic) is not stored: the
+// select and sum passes then re-scan the rows. Distances are binary32 here (the
+// estimate is a statistical quantity: the reference's photon maps come from
+// drand48); the sums are binary64.
 constexpr int kEstCap = 1024;
 
 struct EstLds {
@@ -230,29 +103,70 @@ __device__ __forceinline__ unsigned est_key(float d2, float inv_r2) {
     return q >= 16777215.0f ? 16777215u : (unsigned)q;
 }
 
-// the neighbour cells (lane c < 27 owns cell c, dz outer, dx inner; each bucket once):
-// calls f(p, in, d2) for every chunk of up to 64 consecutive photons of a cell, in
-// uniform control flow; `in`: this lane's photon exists and lies within the radius
+// The candidates of a query at x: every photon whose binary32 distance to x is
+// below the radius lies within `re` of x (the radius widened by the binary32
+// rounding of the positions), hence in a grid row (y, z) whose cell rectangle
+// is within re of (x_y, x_z), at an x-cell within the chord sqrt(re^2 - d_yz^2).
+// Rows are taken 64 at a time (lane l owns row l of the round); their photon
+// ranges are concatenated and scanned in chunks of 64 consecutive candidates,
+// a lane finding its row by binary search over the wave's inclusive prefix of
+// the row lengths, so short rows leave no lanes idle. Calls f(p, in, d2) per
+// chunk in uniform control flow; `in`: this lane's candidate exists and lies
+// within the radius. The visiting order (rows in (z, y) order, photons in grid
+// order) is the same in every pass.
 template <typename F>
-__device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, float r2f, F&& f) {
+__device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, double r, float r2f, F&& f) {
     const int lane = est_lane();
-    const int ci = lane < 27 ? lane : 0;
-    int64_t c[3];
-    for (int k = 0; k < 3; ++k) c[k] = (int64_t)floor((x[k] - M.origin[k]) / M.cell);
-    const uint32_t b = grid_bucket(c[0] + ci % 3 - 1, c[1] + (ci / 3) % 3 - 1, c[2] + ci / 9 - 1, M.num_buckets);
-    bool dup = false;
-    for (int j = 0; j < 26; ++j) {
-        const uint32_t bj = (uint32_t)__shfl((int)b, j, 64);
-        dup = dup || (j < ci && bj == b);
+    const double ax = fmax(fmax(fabs(x[0]), fabs(x[1])), fabs(x[2]));
+    const double re = r * (1.0 + 1e-5) + 0x1p-20 * ax;
+    int lo[3], hi[3];
+    bool any = true;
+    for (int k = 0; k < 3; ++k) {
+        const double a = floor((x[k] - re - M.origin[k]) * M.inv_cell);
+        const double b = floor((x[k] + re - M.origin[k]) * M.inv_cell);
+        const double top = (double)(M.dims[k] - 1);
+        any = any && b >= 0.0 && a <= top;  // (false for NaN)
+        lo[k] = (int)fmin(fmax(a, 0.0), top);
+        hi[k] = (int)fmin(fmax(b, 0.0), top);
     }
-    const bool keep = lane < 27 && !dup;
-    const int32_t s0 = keep ? M.start[b] : 0, e0 = keep ? M.start[b + 1] : 0;
+    if (!any) return;
+    const int ny = hi[1] - lo[1] + 1;
+    const int nrows = ny * (hi[2] - lo[2] + 1);
     const float xf[3] = {(float)x[0], (float)x[1], (float)x[2]};
-    for (int q = 0; q < 27; ++q) {
-        const int32_t s = __builtin_amdgcn_readlane(s0, q), e = __builtin_amdgcn_readlane(e0, q);
-        for (int32_t base = s; base < e; base += 64) {
-            const int32_t p = base + lane;
-            bool in = p < e;
+    for (int rb = 0; rb < nrows; rb += 64) {
+        const int l = rb + lane;
+        int32_t s = 0, cnt = 0;
+        if (l < nrows) {
+            const int iy = lo[1] + l % ny, iz = lo[2] + l / ny;
+            const double ylo = M.origin[1] + (double)iy * M.cell, zlo = M.origin[2] + (double)iz * M.cell;
+            const double dy = fmax(0.0, fmax(ylo - x[1], x[1] - (ylo + M.cell)));
+            const double dz = fmax(0.0, fmax(zlo - x[2], x[2] - (zlo + M.cell)));
+            const double h2 = re * re - dy * dy - dz * dz;
+            if (h2 >= 0.0) {
+                const double hx = sqrt(h2);
+                const double a = floor((x[0] - hx - M.origin[0]) * M.inv_cell);
+                const double b = floor((x[0] + hx - M.origin[0]) * M.inv_cell);
+                const int x0 = (int)fmax(a, (double)lo[0]), x1 = (int)fmin(b, (double)hi[0]);
+                if (x0 <= x1) {
+                    const int64_t row = ((int64_t)iz * M.dims[1] + iy) * (int64_t)M.dims[0];
+                    s = M.start[row + x0];
+                    cnt = M.start[row + x1 + 1] - s;
+                }
+            }
+        }
+        const unsigned incl = wave_incl_scan((unsigned)cnt);
+        const int32_t off = s - (int32_t)(incl - (unsigned)cnt);  // candidate g of this row is photon off + g
+        const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
+        for (unsigned base = 0; base < total; base += 64) {
+            const unsigned g = base + (unsigned)lane;
+            int row = 0;  // the number of rows ending at or before g
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1) {
+                const unsigned e = (unsigned)__shfl((int)incl, row + step - 1, 64);
+                if (e <= g) row += step;
+            }
+            const int32_t p = __shfl(off, row, 64) + (int32_t)g;
+            bool in = g < total;
             float d2 = 0.0f;
             if (in) {
                 const float4 pp = reinterpret_cast<const float4*>(M.pos4)[p];
@@ -290,7 +204,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     const float r2f = (float)r2, inv_r2 = (float)(1.0 / r2);
     // pass 1: the photons within the radius, compacted into the LDS list in scan order
     unsigned total = 0;
-    wave_scan_cells(M, x, r2f, [&](int32_t p, bool in, float d2) {
+    wave_scan_cells(M, x, max_dist, r2f, [&](int32_t p, bool in, float d2) {
         const unsigned long long m = __ballot(in);
         if (in) {
             const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
@@ -314,7 +228,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
                 fn(in ? L.idx[i] : 0, in, in ? L.d2[i] : 0.0f);
             }
         } else {
-            wave_scan_cells(M, x, r2f, fn);
+            wave_scan_cells(M, x, max_dist, r2f, fn);
         }
     };
     // the k-th smallest key: radix select, 8 bits per pass
@@ -372,13 +286,14 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         ties += (unsigned)__popcll(tm);
         if (take) {
             dmax = fmaxf(dmax, d2);
-            const double weight = 1.0 - sqrt((double)d2) / cone_r;
-            const double* dd = M.dir + 3 * (int64_t)p;
-            if ((dd[0] * normal[0] + dd[1] * normal[1] + dd[2] * normal[2]) < 0.0) {
-                const double* w3 = M.power + 3 * (int64_t)p;
-                acc[0] += w3[0] * weight;
-                acc[1] += w3[1] * weight;
-                acc[2] += w3[2] * weight;
+            const double weight = 1.0 - (double)sqrtf(d2) / cone_r;
+            // one 48-byte record: power x, y, z, direction x, y, z
+            const double2* rec = reinterpret_cast<const double2*>(M.pwdir) + 3 * (int64_t)p;
+            const double2 a = rec[0], b = rec[1], c = rec[2];
+            if ((b.y * normal[0] + c.x * normal[1] + c.y * normal[2]) < 0.0) {
+                acc[0] += a.x * weight;
+                acc[1] += a.y * weight;
+                acc[2] += b.x * weight;
             }
         }
     });

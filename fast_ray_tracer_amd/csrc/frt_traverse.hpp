@@ -75,18 +75,20 @@ __device__ __forceinline__ void frame_cache(const Ray& r, FrameCache& c) {
     c.dmax = fmaxf(fmaxf(fabsf(c.df[0]), fabsf(c.df[1])), fabsf(c.df[2]));
 }
 
-// one photon map (frt_gi.hpp): photons sorted by grid bucket (SoA), built on the host after tracing
+// one photon map (frt_gi.hpp): photons sorted by cell of a dense uniform grid
+// (x fastest, so a row of cells is one contiguous photon range), built on the
+// host after tracing
 struct PhotonMapDev {
     const float* pos4;    // 4 per photon: binary32 x, y, z, 0 (the estimate's candidate scan)
-    const double* pos;    // 3 per photon
-    const double* power;  // 3 per photon (scaled by 1 / photon_count)
-    const double* dir;    // 3 per photon: pm_photon_dir of the stored theta / phi bytes (pm.c:80-88)
-    const int32_t* start; // bucket -> first photon, num_buckets + 1 entries
+    const double* pwdir;  // 6 per photon: power (scaled by 1 / photon_count), then pm_photon_dir of
+                          // the stored theta / phi bytes (pm.c:80-88)
+    const int32_t* start; // cell -> first photon, cells + 1 entries
     int64_t count;
-    int32_t num_buckets;  // power of two
+    int32_t dims[3];      // cells per axis
     int32_t pad;
-    double origin[3];     // grid origin
-    double cell;          // cell edge = the estimate's radius
+    double origin[3];     // grid origin (the photons' lower bounding-box corner)
+    double cell;          // cell edge: radius / 3, doubled until the grid fits kMaxGridCells
+    double inv_cell;
 };
 
 struct DevScene {
