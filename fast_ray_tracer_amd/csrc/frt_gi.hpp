@@ -155,26 +155,48 @@ __device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, d
             }
         }
         const unsigned incl = wave_incl_scan((unsigned)cnt);
-        const int32_t off = s - (int32_t)(incl - (unsigned)cnt);  // candidate g of this row is photon off + g
+        const unsigned excl = incl - (unsigned)cnt;
+        const int32_t off = s - (int32_t)excl;  // candidate g of this row is photon off + g
         const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
-        for (unsigned base = 0; base < total; base += 64) {
+        // the row of each candidate: the non-empty rows are visited in order with scalar
+        // reads of their start (no cross-lane permutes); cur_off = the row holding the
+        // chunk's first candidate
+        unsigned long long rest = __ballot(cnt > 0);
+        int32_t cur_off = 0;
+        auto chunk_photon = [&](unsigned base) {
             const unsigned g = base + (unsigned)lane;
-            int row = 0;  // the number of rows ending at or before g
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1) {
-                const unsigned e = (unsigned)__shfl((int)incl, row + step - 1, 64);
-                if (e <= g) row += step;
+            int32_t o = cur_off;
+            while (rest) {
+                const int r = __builtin_ctzll(rest);
+                const unsigned st = (unsigned)__builtin_amdgcn_readlane((int)excl, r);
+                if (st >= base + 64u) break;
+                const int32_t ro = __builtin_amdgcn_readlane(off, r);
+                if (g >= st) o = ro;
+                cur_off = ro;
+                rest &= rest - 1;
             }
-            const int32_t p = __shfl(off, row, 64) + (int32_t)g;
-            bool in = g < total;
-            float d2 = 0.0f;
-            if (in) {
-                const float4 pp = reinterpret_cast<const float4*>(M.pos4)[p];
-                const float dx = pp.x - xf[0], dy = pp.y - xf[1], dz = pp.z - xf[2];
-                d2 = dx * dx + dy * dy + dz * dz;
-                in = d2 < r2f;
+            return o + (int32_t)g;
+        };
+        // two chunks per step: both position loads are in flight before either is used
+        for (unsigned base = 0; base < total; base += 128) {
+            const int32_t pa = chunk_photon(base), pb = chunk_photon(base + 64u);
+            bool ina = base + (unsigned)lane < total, inb = base + 64u + (unsigned)lane < total;
+            float4 qa = make_float4(0.0f, 0.0f, 0.0f, 0.0f), qb = qa;
+            if (ina) qa = reinterpret_cast<const float4*>(M.pos4)[pa];
+            if (inb) qb = reinterpret_cast<const float4*>(M.pos4)[pb];
+            float d2a = 0.0f, d2b = 0.0f;
+            if (ina) {
+                const float dx = qa.x - xf[0], dy = qa.y - xf[1], dz = qa.z - xf[2];
+                d2a = dx * dx + dy * dy + dz * dz;
+                ina = d2a < r2f;
             }
-            f(p, in, d2);
+            if (inb) {
+                const float dx = qb.x - xf[0], dy = qb.y - xf[1], dz = qb.z - xf[2];
+                d2b = dx * dx + dy * dy + dz * dz;
+                inb = d2b < r2f;
+            }
+            f(pa, ina, d2a);
+            f(pb, inb, d2b);
         }
     }
 }
@@ -277,26 +299,53 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     float dmax = 0.0f;
     unsigned ties = 0;
     const bool all = total <= (unsigned)k;
-    visit([&](int32_t p, bool in, float d2) {
+    auto decide = [&](bool in, float d2) {
         const unsigned key = est_key(d2, inv_r2);
         const bool lower = in && (all || (key & mask) < prefix);
         const bool tie = in && !all && (key & mask) == prefix;
         const unsigned long long tm = __ballot(tie);
         const bool take = lower || (tie && (resolved || ties + (unsigned)__popcll(tm & ((1ull << lane) - 1)) < need));
         ties += (unsigned)__popcll(tm);
-        if (take) {
-            dmax = fmaxf(dmax, d2);
-            const double weight = 1.0 - (double)sqrtf(d2) / cone_r;
-            // one 48-byte record: power x, y, z, direction x, y, z
-            const double2* rec = reinterpret_cast<const double2*>(M.pwdir) + 3 * (int64_t)p;
-            const double2 a = rec[0], b = rec[1], c = rec[2];
-            if ((b.y * normal[0] + c.x * normal[1] + c.y * normal[2]) < 0.0) {
-                acc[0] += a.x * weight;
-                acc[1] += a.y * weight;
-                acc[2] += b.x * weight;
-            }
+        return take;
+    };
+    // one 48-byte record per photon: power x, y, z, direction x, y, z
+    auto record = [&](int32_t p, double2* r) {
+        const double2* rec = reinterpret_cast<const double2*>(M.pwdir) + 3 * (int64_t)p;
+        r[0] = rec[0];
+        r[1] = rec[1];
+        r[2] = rec[2];
+    };
+    auto accumulate = [&](float d2, const double2* r) {
+        dmax = fmaxf(dmax, d2);
+        const double weight = 1.0 - (double)sqrtf(d2) / cone_r;
+        if ((r[1].y * normal[0] + r[2].x * normal[1] + r[2].y * normal[2]) < 0.0) {
+            acc[0] += r[0].x * weight;
+            acc[1] += r[0].y * weight;
+            acc[2] += r[1].x * weight;
         }
-    });
+    };
+    if (listed) {  // two chunks per step: both record loads in flight together
+        for (unsigned base = 0; base < total; base += 128) {
+            const unsigned ia = base + (unsigned)lane, ib = ia + 64u;
+            const bool ina = ia < total, inb = ib < total;
+            const int32_t pa = ina ? L.idx[ia] : 0, pb = inb ? L.idx[ib] : 0;
+            const float d2a = ina ? L.d2[ia] : 0.0f, d2b = inb ? L.d2[ib] : 0.0f;
+            const bool ta = decide(ina, d2a), tb = decide(inb, d2b);
+            double2 ra[3], rb[3];
+            if (ta) record(pa, ra);
+            if (tb) record(pb, rb);
+            if (ta) accumulate(d2a, ra);
+            if (tb) accumulate(d2b, rb);
+        }
+    } else {
+        wave_scan_cells(M, x, max_dist, r2f, [&](int32_t p, bool in, float d2) {
+            if (decide(in, d2)) {
+                double2 r[3];
+                record(p, r);
+                accumulate(d2, r);
+            }
+        });
+    }
     for (int j = 0; j < 3; ++j) irrad[j] = wave_sum_d(acc[j]);
     dmax = wave_max_f(dmax);
     EST_STAMP(2);
