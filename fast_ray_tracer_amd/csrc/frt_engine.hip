@@ -812,6 +812,13 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
     __shared__ unsigned name##_hist[kBlock / 64][256];                       \
     const EstLds name{name##_d2[threadIdx.x >> 6], name##_idx[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6]}
 
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // the lanes' estimate requests one after another, each by the whole wave; every lane of the
 // wave must call this at the same point. est: this lane's scaled estimate (photon_estimate)
 __device__ inline void wave_photon_estimates(const PhotonMapDev& M, const DevScene& S, bool want, const double* point,
@@ -822,9 +829,9 @@ __device__ inline void wave_photon_estimates(const PhotonMapDev& M, const DevSce
         const int j = __builtin_ctzll(reqs);
         reqs &= reqs - 1;
         double x[3], nrm[3], e[3];
-        for (int k = 0; k < 3; ++k) {
-            x[k] = __shfl(point[k], j, 64);
-            nrm[k] = __shfl(eyev[k], j, 64);
+        for (int k = 0; k < 3; ++k) {  // wave-uniform: scalar registers
+            x[k] = readlane_d(point[k], j);
+            nrm[k] = readlane_d(eyev[k], j);
         }
         // the reference passes eyev as the estimate's normal (renderer.c:875)
         const int64_t used = wave_irradiance_estimate(M, x, nrm, S.cfg.irradiance_radius, S.cfg.irradiance_num,
@@ -904,18 +911,26 @@ __global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed
     gq[t] = qr;
 }
 
-// color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray, scaled by the sample's
-// first coordinate (final_gather: "scale by theta"); the photon estimates wave-cooperatively
+// what the final gather's estimate needs of one gather ray's hit (k_gather_hit -> k_gather_est)
+struct GatherReq {
+    double pt[3], ev[3];  // lighting_gi's estimate point (over_point) and "normal" (eyev)
+    double kd[3], edn;    // over_Kd, eyev . normalv
+    double jit0;          // the sample's first coordinate (final_gather: "scale by theta")
+    int32_t want, pad;
+};
+
+// color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray up to the estimate: the
+// hit's prepare_computations and material, written as a GatherReq
 template <bool kPat>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) k_gather_shade(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
-                                                         const HitRec* __restrict__ hits, int64_t n,
-                                                         double* __restrict__ gather_col) {
-    FRT_EST_LDS(lds);
+__global__ void __launch_bounds__(kBlock) k_gather_hit(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
+                                                       const HitRec* __restrict__ hits, int64_t n,
+                                                       GatherReq* __restrict__ req) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
     bool want = false;
     double pt[3] = {0, 0, 0}, ev[3] = {0, 0, 0}, kd[3] = {0, 0, 0}, edn = 0.0;
     QueuedRay qr{};
-    if (t < n) {
+    {
         qr = gq[t];
         const HitRec hr = hits[t];
         if (qr.parent >= 0 && hr.node >= 0) {
@@ -946,26 +961,58 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 
             }
         }
     }
-    double est[3];
-    wave_photon_estimates(S.pmaps[1], S, want, pt, ev, 10.0 * (double)S.cfg.irradiance_num, est, lds);
-    if (t >= n) return;
-    double out3[3] = {0, 0, 0};
-    if (want) {
-        if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
-            for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
-        } else {
-            for (int k = 0; k < 3; ++k) {
-                double dk = kd[k] * est[k];
-                dk = dk * edn;
-                out3[k] = dk * kPi;  // shade_hit_gi: x pi
-            }
-        }
-    }
     double jit[2];
     cmj_point(seed ^ kTagGather, qr.key, S.cfg.gi_usteps, S.cfg.gi_vsteps, qr.slot % S.cfg.gi_usteps,
               qr.slot / S.cfg.gi_usteps, jit);
+    GatherReq r;
+    for (int k = 0; k < 3; ++k) {
+        r.pt[k] = pt[k];
+        r.ev[k] = ev[k];
+        r.kd[k] = kd[k];
+    }
+    r.edn = edn;
+    r.jit0 = jit[0];
+    r.want = want ? 1 : 0;
+    r.pad = 0;
+    req[t] = r;
+}
+
+// the gather hits' photon estimates (lighting_gi, renderer.c:863-892), wave-cooperatively, in a
+// kernel that holds only the estimate's state (the hit shading above needs far more registers)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n,
+                                                       double* __restrict__ gather_col) {
+    FRT_EST_LDS(lds);
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool want = false;
+    double pt[3] = {0, 0, 0}, ev[3] = {0, 0, 0};
+    if (t < n) {
+        const GatherReq& r = req[t];
+        want = r.want != 0;
+        for (int k = 0; k < 3; ++k) {
+            pt[k] = r.pt[k];
+            ev[k] = r.ev[k];
+        }
+    }
+    double est[3];
+    wave_photon_estimates(S.pmaps[1], S, want, pt, ev, 10.0 * (double)S.cfg.irradiance_num, est, lds);
+    if (t >= n) return;
     double* out = gather_col + 3 * t;
-    for (int k = 0; k < 3; ++k) out[k] = out3[k] * jit[0];
+    if (!want) {
+        for (int k = 0; k < 3; ++k) out[k] = 0.0;
+        return;
+    }
+    const GatherReq& r = req[t];
+    double out3[3];
+    if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
+        for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
+    } else {
+        for (int k = 0; k < 3; ++k) {
+            double dk = r.kd[k] * est[k];
+            dk = dk * r.edn;
+            out3[k] = dk * kPi;  // shade_hit_gi: x pi
+        }
+    }
+    for (int k = 0; k < 3; ++k) out[k] = out3[k] * r.jit0;
 }
 
 // final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd
@@ -1079,7 +1126,8 @@ struct frt_scene_handle {
         frt::QueuedRay* gq = nullptr;
         frt::HitRec* ghits = nullptr;
         double* gcol = nullptr;
-        int64_t gq_cap = 0, ghits_cap = 0, gcol_cap = 0;
+        frt::GatherReq* greq = nullptr;
+        int64_t gq_cap = 0, ghits_cap = 0, gcol_cap = 0, greq_cap = 0;
         double* extra = nullptr;
         double* fgather = nullptr;
         int64_t extra_cap = 0, fgather_cap = 0;
@@ -1483,6 +1531,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(G.gq));
         hip_ignore(hipFree(G.ghits));
         hip_ignore(hipFree(G.gcol));
+        hip_ignore(hipFree(G.greq));
         hip_ignore(hipFree(G.extra));
         hip_ignore(hipFree(G.fgather));
     }
@@ -1857,15 +1906,18 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
         for (int64_t n0 = 0; n0 < n; n0 += chunk) {
             const int64_t m = std::min(chunk, n - n0);
             const int64_t rays = m * rays_per;
-            if (grow(&G.gq, G.gq_cap, rays) || grow(&G.ghits, G.ghits_cap, rays) || grow(&G.gcol, G.gcol_cap, 3 * rays))
+            if (grow(&G.gq, G.gq_cap, rays) || grow(&G.ghits, G.ghits_cap, rays) || grow(&G.gcol, G.gcol_cap, 3 * rays) ||
+                grow(&G.greq, G.greq_cap, rays))
                 return -1;
             hipLaunchKernelGGL(k_gather_gen, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, L.rec, n0, m,
                                G.gq);
             frt::Batch Bg = B;  // the gather rays form one contiguous queue
             Bg.qprefix = nullptr;
             launch_trace(h, Bg, G.gq, rays, G.ghits, 0);
-            hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_gather_shade<true> : k_gather_shade<false>, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq,
-                               G.ghits, rays, G.gcol);
+            hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_gather_hit<true> : k_gather_hit<false>, dim3(grid_for(rays)),
+                               dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq, G.ghits, rays, G.greq);
+            hipLaunchKernelGGL(k_gather_est, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, G.greq, rays,
+                               G.gcol);
             hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
                                G.fgather);
             FRT_HIP(hipGetLastError());
