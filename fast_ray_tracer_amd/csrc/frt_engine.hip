@@ -806,11 +806,12 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
 }
 
 // the wave's LDS for wave_irradiance_estimate (frt_gi.hpp); blocks of kBlock threads
-#define FRT_EST_LDS(name)                                                    \
-    __shared__ float name##_d2[kBlock / 64][kEstCap];                        \
-    __shared__ int32_t name##_idx[kBlock / 64][kEstCap];                     \
+#define FRT_EST_LDS(name, cap)                                               \
+    __shared__ float name##_d2[kBlock / 64][cap];                            \
+    __shared__ int32_t name##_idx[kBlock / 64][cap];                         \
     __shared__ unsigned name##_hist[kBlock / 64][256];                       \
-    const EstLds name{name##_d2[threadIdx.x >> 6], name##_idx[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6]}
+    const EstLds name{name##_d2[threadIdx.x >> 6], name##_idx[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6], \
+                      (unsigned)(cap)}
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -847,7 +848,7 @@ __device__ inline void wave_photon_estimates(const PhotonMapDev& M, const DevSce
 // per shaded node: the visualisation term (lighting_gi) and the caustics term (renderer.c:740-761)
 __global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, Cols<NodeRec> rec, int64_t n,
                                                     double* __restrict__ gi_extra) {
-    FRT_EST_LDS(lds);
+    FRT_EST_LDS(lds, kEstCap);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     NodeRec nr{};
     bool want = false;
@@ -977,42 +978,49 @@ __global__ void __launch_bounds__(kBlock) k_gather_hit(DevScene S, uint64_t seed
     req[t] = r;
 }
 
-// the gather hits' photon estimates (lighting_gi, renderer.c:863-892), wave-cooperatively, in a
-// kernel that holds only the estimate's state (the hit shading above needs far more registers)
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n,
-                                                       double* __restrict__ gather_col) {
-    FRT_EST_LDS(lds);
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool want = false;
-    double pt[3] = {0, 0, 0}, ev[3] = {0, 0, 0};
-    if (t < n) {
-        const GatherReq& r = req[t];
-        want = r.want != 0;
+// the gather hits' photon estimates (lighting_gi, renderer.c:863-892) in a kernel that holds only
+// the estimate's state: the wave takes its 64 requests one after another, each read through the
+// scalar cache (wave-uniform address), and lane j keeps request j's result for one coalesced store.
+// LDS list capacity kGatherEstCap and <= 96 VGPRs: five waves per SIMD
+constexpr int kGatherEstCap = 768;
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) k_gather_est(
+    DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col) {
+    FRT_EST_LDS(lds, kGatherEstCap);
+    const int lane = est_lane();
+    const int64_t base = (int64_t)blockIdx.x * blockDim.x + 64 * __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const double scale_num = 10.0 * (double)S.cfg.irradiance_num;
+    double mine[3] = {0.0, 0.0, 0.0};
+    for (int j = 0; j < 64 && base + j < n; ++j) {
+        const GatherReq& r = req[base + j];
+        if (!r.want) continue;
+        double x[3], nrm[3], e[3], est[3] = {0.0, 0.0, 0.0};
         for (int k = 0; k < 3; ++k) {
-            pt[k] = r.pt[k];
-            ev[k] = r.ev[k];
+            x[k] = r.pt[k];
+            nrm[k] = r.ev[k];  // the reference passes eyev as the estimate's normal (renderer.c:875)
         }
-    }
-    double est[3];
-    wave_photon_estimates(S.pmaps[1], S, want, pt, ev, 10.0 * (double)S.cfg.irradiance_num, est, lds);
-    if (t >= n) return;
-    double* out = gather_col + 3 * t;
-    if (!want) {
-        for (int k = 0; k < 3; ++k) out[k] = 0.0;
-        return;
-    }
-    const GatherReq& r = req[t];
-    double out3[3];
-    if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
-        for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
-    } else {
-        for (int k = 0; k < 3; ++k) {
-            double dk = r.kd[k] * est[k];
-            dk = dk * r.edn;
-            out3[k] = dk * kPi;  // shade_hit_gi: x pi
+        const int64_t used = wave_irradiance_estimate(S.pmaps[1], x, nrm, S.cfg.irradiance_radius, S.cfg.irradiance_num,
+                                                      S.cfg.cone_filter_k, e, lds,
+                                                      S.dbg ? S.dbg + kDbgProf + 13 : nullptr);
+        if (used > 0) {
+            const double f = scale_num / (double)used;
+            for (int k = 0; k < 3; ++k) est[k] = e[k] * f;
         }
+        double out3[3];
+        if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
+            for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
+        } else {
+            for (int k = 0; k < 3; ++k) {
+                double dk = r.kd[k] * est[k];
+                dk = dk * r.edn;
+                out3[k] = dk * kPi;  // shade_hit_gi: x pi
+            }
+        }
+        if (lane == j)
+            for (int k = 0; k < 3; ++k) mine[k] = out3[k] * r.jit0;
     }
-    for (int k = 0; k < 3; ++k) out[k] = out3[k] * r.jit0;
+    const int64_t t = base + lane;
+    if (t < n)
+        for (int k = 0; k < 3; ++k) gather_col[3 * t + k] = mine[k];
 }
 
 // final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd

@@ -62,16 +62,17 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
 // the wave's LDS list (ballot + rank), the k-th smallest distance is found by a
 // radix select over 24-bit keys of d^2 / r^2 (LDS histograms, at most three
 // passes over the list), and the cone-filtered sum is one more pass with a wave
-// reduction. A list longer than kEstCap (a dense caustic) is not stored: the
+// reduction. A list longer than the wave's capacity (a dense caustic) is not stored: the
 // select and sum passes then re-scan the rows. Distances are binary32 here (the
 // estimate is a statistical quantity: the reference's photon maps come from
 // drand48); the sums are binary64.
 constexpr int kEstCap = 1024;
 
 struct EstLds {
-    float* d2;        // kEstCap: squared distances of the photons within the radius
-    int32_t* idx;     // kEstCap: their photon indices
+    float* d2;        // cap: squared distances of the photons within the radius
+    int32_t* idx;     // cap: their photon indices
     unsigned* hist;   // 256
+    unsigned cap;
 };
 
 __device__ __forceinline__ int est_lane() { return (int)(threadIdx.x & 63); }
@@ -108,9 +109,9 @@ __device__ __forceinline__ unsigned est_key(float d2, float inv_r2) {
 // rounding of the positions), hence in a grid row (y, z) whose cell rectangle
 // is within re of (x_y, x_z), at an x-cell within the chord sqrt(re^2 - d_yz^2).
 // Rows are taken 64 at a time (lane l owns row l of the round); their photon
-// ranges are concatenated and scanned in chunks of 64 consecutive candidates,
-// a lane finding its row by binary search over the wave's inclusive prefix of
-// the row lengths, so short rows leave no lanes idle. Calls f(p, in, d2) per
+// ranges are concatenated and scanned in chunks of 64 consecutive candidates
+// (the rows starting inside a chunk are read with scalar readlanes), so short
+// rows leave no lanes idle. Calls f(p, in, d2) per
 // chunk in uniform control flow; `in`: this lane's candidate exists and lies
 // within the radius. The visiting order (rows in (z, y) order, photons in grid
 // order) is the same in every pass.
@@ -230,7 +231,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         const unsigned long long m = __ballot(in);
         if (in) {
             const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
-            if (at < (unsigned)kEstCap) {
+            if (at < L.cap) {
                 L.d2[at] = d2;
                 L.idx[at] = p;
             }
@@ -240,7 +241,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     EST_STAMP(0);
     const unsigned found = total < (unsigned)k ? total : (unsigned)k;
     if (found < 8) return found;
-    const bool listed = total <= (unsigned)kEstCap;
+    const bool listed = total <= L.cap;
     // every pass visits the in-range photons in the same order: from the list, or a re-scan
     auto visit = [&](auto&& fn) {
         if (listed) {
