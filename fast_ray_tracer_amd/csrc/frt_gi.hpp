@@ -60,8 +60,8 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
 // sphere's chord, are concatenated and scanned 64 photons at a time
 // (coalesced binary32 positions); photons within the radius are compacted into
 // the wave's LDS list (ballot + rank), the k-th smallest distance is found by a
-// radix select over 24-bit keys of d^2 / r^2 (LDS histograms, at most three
-// passes over the list), and the cone-filtered sum is one more pass with a wave
+// radix select over 24-bit keys of d^2 / r^2 (LDS histograms: the first digit's
+// built during the scan, at most two more passes over the list), and the cone-filtered sum is one more pass with a wave
 // reduction. A list longer than the wave's capacity (a dense caustic) is not stored: the
 // select and sum passes then re-scan the rows. Distances are binary32 here (the
 // estimate is a statistical quantity: the reference's photon maps come from
@@ -225,7 +225,10 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     const int lane = est_lane();
     const double r2 = max_dist * max_dist;
     const float r2f = (float)r2, inv_r2 = (float)(1.0 / r2);
-    // pass 1: the photons within the radius, compacted into the LDS list in scan order
+    // pass 1: the photons within the radius, compacted into the LDS list in scan order, and the
+    // histogram of their keys' top byte (the radix select's first digit)
+    for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+    __builtin_amdgcn_wave_barrier();
     unsigned total = 0;
     wave_scan_cells(M, x, max_dist, r2f, [&](int32_t p, bool in, float d2) {
         const unsigned long long m = __ballot(in);
@@ -235,6 +238,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
                 L.d2[at] = d2;
                 L.idx[at] = p;
             }
+            atomicAdd(&L.hist[est_key(d2, inv_r2) >> 16], 1u);
         }
         total += (unsigned)__popcll(m);
     });
@@ -258,12 +262,14 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     unsigned prefix = 0, mask = 0, need = found;
     bool resolved = total <= (unsigned)k;  // every photon in range is used
     for (int shift = 16; shift >= 0 && !resolved; shift -= 8) {
-        for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
-        __builtin_amdgcn_wave_barrier();
-        visit([&](int32_t, bool in, float d2) {
-            const unsigned key = est_key(d2, inv_r2);
-            if (in && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
-        });
+        if (shift != 16) {  // (the first digit's histogram came with pass 1)
+            for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+            __builtin_amdgcn_wave_barrier();
+            visit([&](int32_t, bool in, float d2) {
+                const unsigned key = est_key(d2, inv_r2);
+                if (in && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
+            });
+        }
         __builtin_amdgcn_wave_barrier();
         unsigned h4[4], local = 0;
         for (int j = 0; j < 4; ++j) {
