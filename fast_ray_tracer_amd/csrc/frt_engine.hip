@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "frt_device.h"
@@ -1709,6 +1710,33 @@ static uint64_t host_mix64(uint64_t x) {  // frt::mix64 on the host
 // follows the measured store rate. The reference loops forever when a light
 // can store nothing (no diffuse surface reachable); here the emission count is
 // bounded and the map keeps what was found.
+// the order of the stored photons by key (emission index << 8 | bounce, unique): LSD radix sort
+// over 16-bit digits of (key, index) pairs, instead of sorting the 80-byte records
+static std::vector<uint32_t> key_order(const std::vector<frt::StoredPhoton>& a) {
+    const size_t n = a.size();
+    std::vector<uint64_t> k(n), k2(n);
+    std::vector<uint32_t> idx(n), idx2(n), cnt((size_t)65536 + 1);
+    uint64_t mx = 0;
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = a[i].key;
+        idx[i] = (uint32_t)i;
+        mx = std::max(mx, k[i]);
+    }
+    for (int shift = 0; shift < 64 && (mx >> shift) != 0; shift += 16) {
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        for (size_t i = 0; i < n; ++i) cnt[((k[i] >> shift) & 0xffff) + 1]++;
+        for (size_t d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t at = cnt[(k[i] >> shift) & 0xffff]++;
+            k2[at] = k[i];
+            idx2[at] = idx[i];
+        }
+        k.swap(k2);
+        idx.swap(idx2);
+    }
+    return idx;
+}
+
 static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t seed,
                                std::vector<frt::StoredPhoton>& out) {
     using namespace frt;
@@ -1766,15 +1794,17 @@ static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t
         batch = rate > 0 ? (int64_t)std::min<double>((double)kMaxBatch, need / rate * 1.25 + 1024.0)
                          : std::min<int64_t>(batch * 4, kMaxBatch);
     }
-    std::sort(acc.begin(), acc.end(), [](const StoredPhoton& a, const StoredPhoton& b) { return a.key < b.key; });
+    // the reference's storage order: by emission, then bounce
+    const std::vector<uint32_t> ord = key_order(acc);
     // keep the emissions up to the first one at which the count reaches `want`
     size_t keep = acc.size();
     if ((int64_t)acc.size() >= want) {
-        const uint64_t last = acc[(size_t)want - 1].key >> 8;
+        const uint64_t last = acc[ord[(size_t)want - 1]].key >> 8;
         keep = (size_t)want;
-        while (keep < acc.size() && (acc[keep].key >> 8) == last) ++keep;
+        while (keep < acc.size() && (acc[ord[keep]].key >> 8) == last) ++keep;
     }
-    out.insert(out.end(), acc.begin(), acc.begin() + (ptrdiff_t)keep);
+    out.reserve(out.size() + keep);
+    for (size_t i = 0; i < keep; ++i) out.push_back(acc[ord[i]]);
     return 0;
 }
 
@@ -1788,10 +1818,23 @@ static void quantized_dir(const double* d, double* out) {
     phi = phi > 255 ? 255 : (phi < 0 ? phi + 256 : phi);
     theta &= 255;
     phi &= 255;
-    const double ta = (double)theta * (1.0 / 256.0) * M_PI, pa = (double)phi * (1.0 / 256.0) * M_PI;
-    out[0] = std::sin(ta) * std::cos(2.0 * pa);
-    out[1] = std::sin(ta) * std::sin(2.0 * pa);
-    out[2] = std::cos(ta);
+    // the decoded angles' sines and cosines, tabulated once (the same expressions per byte value)
+    struct Tables {
+        double st[256], ct[256], c2p[256], s2p[256];
+        Tables() {
+            for (int b = 0; b < 256; ++b) {
+                const double ta = (double)b * (1.0 / 256.0) * M_PI, pa = (double)b * (1.0 / 256.0) * M_PI;
+                st[b] = std::sin(ta);
+                ct[b] = std::cos(ta);
+                c2p[b] = std::cos(2.0 * pa);
+                s2p[b] = std::sin(2.0 * pa);
+            }
+        }
+    };
+    static const Tables T;
+    out[0] = T.st[theta] * T.c2p[phi];
+    out[1] = T.st[theta] * T.s2p[phi];
+    out[2] = T.ct[theta];
 }
 
 // dense uniform grid over the photons (frt_gi.hpp wave_scan_cells): cell edge
@@ -1850,14 +1893,26 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
     }
     for (int64_t b = 0; b < ncells; ++b) start[(size_t)b + 1] += start[(size_t)b];
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    // pm_photon_dir of every photon, on the host's cores (acos / atan2 per photon)
+    std::vector<double> qdir((size_t)n * 3);
+    {
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(), 16,
+                                                                       n / 65536 + 1}));
+        std::vector<std::thread> pool;
+        for (int w = 0; w < nt; ++w)
+            pool.emplace_back([&, w]() {
+                const int64_t i0 = n * w / nt, i1 = n * (w + 1) / nt;
+                for (int64_t i = i0; i < i1; ++i) quantized_dir(ph[(size_t)i].dir, qdir.data() + 3 * i);
+            });
+        for (auto& th : pool) th.join();
+    }
     const size_t np = (size_t)std::max<int64_t>(n, 1);
     std::vector<float> pos4(np * 4, 0.0f);
     std::vector<double> pwdir(np * 6, 0.0);
     for (int64_t i = 0; i < n; ++i) {
         const auto& p = ph[(size_t)i];
         const int64_t j = fill[(size_t)cell_of[(size_t)i]]++;
-        double d[3];
-        quantized_dir(p.dir, d);
+        const double* d = qdir.data() + 3 * i;
         for (int k = 0; k < 3; ++k) {
             pos4[(size_t)(4 * j + k)] = (float)p.pos[k];
             pwdir[(size_t)(6 * j + k)] = p.power[k] * scale;  // pm_scale_photon_power
