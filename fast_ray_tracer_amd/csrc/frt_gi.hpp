@@ -61,8 +61,9 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
 // (coalesced binary32 positions); photons within the radius are compacted into
 // the wave's LDS list (ballot + rank), the k-th smallest distance is found by a
 // radix select over 24-bit keys of d^2 / r^2 (LDS histograms: the first digit's
-// built during the scan, at most two more passes over the list), and the cone-filtered sum is one more pass with a wave
-// reduction. A list longer than the wave's capacity (a dense caustic) is not stored: the
+// built during the scan; when the k-th falls in a bin of at most 64 photons they
+// are ranked directly in the sum pass, else up to two more passes over the
+// list), and the cone-filtered sum is one more pass with a wave reduction. A list longer than the wave's capacity (a dense caustic) is not stored: the
 // select and sum passes then re-scan the rows. Distances are binary32 here (the
 // estimate is a statistical quantity: the reference's photon maps come from
 // drand48); the sums are binary64.
@@ -261,6 +262,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     // the k-th smallest key: radix select, 8 bits per pass
     unsigned prefix = 0, mask = 0, need = found;
     bool resolved = total <= (unsigned)k;  // every photon in range is used
+    bool few_ties = false;  // the k-th lies among <= 64 photons of one bin: ranked directly in the sum pass
     for (int shift = 16; shift >= 0 && !resolved; shift -= 8) {
         if (shift != 16) {  // (the first digit's histogram came with pass 1)
             for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
@@ -298,6 +300,10 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         prefix |= (unsigned)bin << shift;
         mask |= 255u << shift;
         resolved = cnt == need;
+        if (!resolved && cnt <= 64u) {
+            few_ties = true;
+            break;
+        }
     }
     EST_STAMP(1);
     // sum pass (pm.c:125-145): keys below the k-th are in; at the k-th key the first `need` met
@@ -306,12 +312,25 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     float dmax = 0.0f;
     unsigned ties = 0;
     const bool all = total <= (unsigned)k;
-    auto decide = [&](bool in, float d2) {
+    // few_ties: the bin's photons (the "ties" at the selected prefix) are set aside in L.hist
+    // (index, d^2, key at scan position r < 64) and the `need` smallest by (key, scan order) taken
+    // after the pass: the same photons as a further select pass would keep
+    auto decide = [&](int32_t p, bool in, float d2) {
         const unsigned key = est_key(d2, inv_r2);
         const bool lower = in && (all || (key & mask) < prefix);
         const bool tie = in && !all && (key & mask) == prefix;
         const unsigned long long tm = __ballot(tie);
-        const bool take = lower || (tie && (resolved || ties + (unsigned)__popcll(tm & ((1ull << lane) - 1)) < need));
+        const unsigned r = ties + (unsigned)__popcll(tm & ((1ull << lane) - 1));
+        bool take = lower;
+        if (few_ties) {
+            if (tie) {
+                L.hist[r] = (unsigned)p;
+                L.hist[64 + r] = __float_as_uint(d2);
+                L.hist[128 + r] = key;
+            }
+        } else {
+            take = take || (tie && (resolved || r < need));
+        }
         ties += (unsigned)__popcll(tm);
         return take;
     };
@@ -337,7 +356,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
             const bool ina = ia < total, inb = ib < total;
             const int32_t pa = ina ? L.idx[ia] : 0, pb = inb ? L.idx[ib] : 0;
             const float d2a = ina ? L.d2[ia] : 0.0f, d2b = inb ? L.d2[ib] : 0.0f;
-            const bool ta = decide(ina, d2a), tb = decide(inb, d2b);
+            const bool ta = decide(pa, ina, d2a), tb = decide(pb, inb, d2b);
             double2 ra[3], rb[3];
             if (ta) record(pa, ra);
             if (tb) record(pb, rb);
@@ -346,12 +365,28 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         }
     } else {
         wave_scan_cells(M, x, max_dist, r2f, [&](int32_t p, bool in, float d2) {
-            if (decide(in, d2)) {
+            if (decide(p, in, d2)) {
                 double2 r[3];
                 record(p, r);
                 accumulate(d2, r);
             }
         });
+    }
+    if (few_ties) {
+        __builtin_amdgcn_wave_barrier();
+        const bool mine = (unsigned)lane < ties;
+        const unsigned kl = mine ? L.hist[128 + lane] : 0xffffffffu;
+        unsigned rank = 0;
+        for (unsigned m = 0; m < ties; ++m) {
+            const unsigned km = (unsigned)__builtin_amdgcn_readlane((int)kl, (int)m);
+            rank += (km < kl || (km == kl && m < (unsigned)lane)) ? 1u : 0u;
+        }
+        if (mine && rank < need) {
+            const float d2 = __uint_as_float(L.hist[64 + lane]);
+            double2 r[3];
+            record((int32_t)L.hist[lane], r);
+            accumulate(d2, r);
+        }
     }
     for (int j = 0; j < 3; ++j) irrad[j] = wave_sum_d(acc[j]);
     dmax = wave_max_f(dmax);
