@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -1938,14 +1939,23 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
 static int build_photon_maps(frt_scene_handle* h, uint64_t seed) {
     const auto& cfg = h->S.cfg;
     const int want[2] = {cfg.trace_caustic_map, cfg.trace_global_map};
+    const bool timing = std::getenv("FRT_GI_TIMING") != nullptr;  // diagnostics: host-side phase times
     for (int m = 0; m < 2; ++m) {
+        const auto t0 = std::chrono::steady_clock::now();
         std::vector<frt::StoredPhoton> ph;
         if (want[m])
             for (int l = 0; l < h->S.num_lights; ++l)
                 if (trace_light_photons(h, m, l, seed, ph)) return -1;
         // pm_store keeps at most max_photons + 1 photons (pm.c:271)
         if ((int64_t)ph.size() > cfg.photon_count + 1) ph.resize((size_t)cfg.photon_count + 1);
+        const auto t1 = std::chrono::steady_clock::now();
         if (build_photon_map(h, m, ph, 1.0 / (double)cfg.photon_count)) return -1;
+        if (timing) {
+            const auto t2 = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "photon map %d: %zu photons, trace %.1f ms, build %.1f ms\n", m, ph.size(),
+                         std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                         std::chrono::duration<double, std::milli>(t2 - t1).count());
+        }
     }
     h->gi.built = true;
     h->gi.seed = seed;
