@@ -809,10 +809,9 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
 
 // the wave's LDS for wave_irradiance_estimate (frt_gi.hpp); blocks of kBlock threads
 #define FRT_EST_LDS(name, cap)                                               \
-    __shared__ float name##_d2[kBlock / 64][cap];                            \
-    __shared__ int32_t name##_idx[kBlock / 64][cap];                         \
+    __shared__ uint2 name##_ent[kBlock / 64][cap];                           \
     __shared__ unsigned name##_hist[kBlock / 64][256];                       \
-    const EstLds name{name##_d2[threadIdx.x >> 6], name##_idx[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6], \
+    const EstLds name{name##_ent[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6],                          \
                       (unsigned)(cap)}
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {

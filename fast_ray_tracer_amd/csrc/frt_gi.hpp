@@ -70,8 +70,7 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
 constexpr int kEstCap = 1024;
 
 struct EstLds {
-    float* d2;        // cap: squared distances of the photons within the radius
-    int32_t* idx;     // cap: their photon indices
+    uint2* ent;       // cap: (squared distance bits, photon index) of the photons within the radius
     unsigned* hist;   // 256
     unsigned cap;
 };
@@ -236,8 +235,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         if (in) {
             const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
             if (at < L.cap) {
-                L.d2[at] = d2;
-                L.idx[at] = p;
+                L.ent[at] = make_uint2(__float_as_uint(d2), (unsigned)p);
             }
             atomicAdd(&L.hist[est_key(d2, inv_r2) >> 16], 1u);
         }
@@ -253,7 +251,8 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
             for (unsigned base = 0; base < total; base += 64) {
                 const unsigned i = base + (unsigned)lane;
                 const bool in = i < total;
-                fn(in ? L.idx[i] : 0, in, in ? L.d2[i] : 0.0f);
+                const uint2 e = in ? L.ent[i] : make_uint2(0u, 0u);
+                fn((int32_t)e.y, in, __uint_as_float(e.x));
             }
         } else {
             wave_scan_cells(M, x, max_dist, r2f, fn);
@@ -354,8 +353,9 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         for (unsigned base = 0; base < total; base += 128) {
             const unsigned ia = base + (unsigned)lane, ib = ia + 64u;
             const bool ina = ia < total, inb = ib < total;
-            const int32_t pa = ina ? L.idx[ia] : 0, pb = inb ? L.idx[ib] : 0;
-            const float d2a = ina ? L.d2[ia] : 0.0f, d2b = inb ? L.d2[ib] : 0.0f;
+            const uint2 ea = ina ? L.ent[ia] : make_uint2(0u, 0u), eb = inb ? L.ent[ib] : make_uint2(0u, 0u);
+            const int32_t pa = (int32_t)ea.y, pb = (int32_t)eb.y;
+            const float d2a = __uint_as_float(ea.x), d2b = __uint_as_float(eb.x);
             const bool ta = decide(pa, ina, d2a), tb = decide(pb, inb, d2b);
             double2 ra[3], rb[3];
             if (ta) record(pa, ra);
