@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """bench.py — frt-mi355x headline benchmark.
 
-Workload (BASELINE.json configs[2]): cornell_box at 800x800 with a 4x4 CMJ
-sub-pixel grid (16 spp), full reflection/refraction recursion (path length 5),
-one 10x10 area light; GI off and a single-row light cache (the deterministic
-parity variant the tests check bit-for-bit against the reference). The scene is
-the reference codegen's own main.c (tests/golden/scenes/), built through the
-drop-in API in capture mode.
+Workload (BASELINE.json north_star target / configs[4] camera): cornell_box at
+1920x1080 with an 8x8 CMJ sub-pixel grid (64 spp), full reflection/refraction
+recursion (path length 5), one 10x10 area light; GI off and a single-row light
+cache — the deterministic parity variant the tests check against the oracle
+(tests/test_gpu_parity.py) and, at 1/64 of the pixels, against the reference
+itself (golden cornell_direct_240x135_8x8). The scene is the reference
+codegen's own main.c (tests/golden/scenes/), built through the drop-in API in
+capture mode.
 
 One step = one full frame: every rank renders its interleaved rows on its GPU
 (HBM-resident output), then the canvas is gathered on rank 0 over RCCL.
@@ -15,14 +17,31 @@ over ranks, plus wall-clock per frame; reference-equivalent Mrays/s (the rays th
 reference would cast, counted by the oracle: zero-weight secondary subtrees
 included) are reported beside it.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--scene NAME] [--no-cpu-baseline]
+Also on the same JSON line:
+  gi               the shipped GI configuration (BASELINE configs[4]: 1M photons per map,
+                   8x8 final gather, k = 200) at 1920x1080x64: --gi-steps frames, each with a
+                   new seed so photon tracing + map build run inside the timed region
+  render_multi_*   wall time of the drop-in entry point itself (flatten, upload, hiprtc
+                   compile of the scene kernel, render, copy to the host canvas)
+  roofline         the dominant kernel (the shadow pass) against HBM peak, with the PMC
+                   traffic / VALU counters committed under profiles/
+  cpu_baseline     the reference's own pthread render_multi on this host's cores, on a
+                   bounded sample of the same workload (the same camera at 240x135)
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--gi-steps G] [--scene NAME] [--no-cpu-baseline]
   torchrun --nproc-per-node N bench.py --gpus N ...
+
+With --gpus N > 1 and no torchrun environment, bench.py starts torchrun itself
+(one rank per GPU) before touching the GPU and exits with its status; a
+WORLD_SIZE that disagrees with --gpus is an error (never a silent 1-GPU run).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -30,52 +49,134 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 ASSETS = os.path.join(GOLDEN, "assets")
-DEFAULT_SCENE = "cornell_direct_800_4x4"
-CPU_SAMPLE_SCENE = "cornell_direct_200_4x4_t16"
+DEFAULT_SCENE = "cornell_direct_1920x1080_8x8"
+GI_SCENE = "cornell_gi_1920x1080_8x8"
+CPU_SAMPLE_SCENE = "cornell_direct_240x135_8x8"
+CPU_SAMPLE_THREADS = 16  # the GPU box's CPU share per GPU (the reference binary's thread-count)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = "r01_pmc_shadow.json"  # tools/profile_round.sh + profile_summary.py: FETCH/WRITE_SIZE, SQ_* of the shadow kernel
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 2 cycles (SIMD32; binary64
 # and transcendental instructions take 2-4x: profiles/r01_microbench_valu.txt) at the 2.4 GHz peak clock
 VALU_PEAK_GINST_S = 1024 * 2.4 / 2.0
 
-# algorithmic HBM bytes of k_shadow ("byte model"), reported by the engine per frame as
-# stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point,
-# key, material; one cache line) and one 4-byte unshadowed count per light it writes. Light points
-# and sample tables (a few KB) stay in cache and are not counted.
+# algorithmic HBM bytes of the shadow kernel ("byte model"), reported by the engine per frame
+# as stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point, key,
+# material; one cache line) and one 4-byte unshadowed count per light it writes. Light points and
+# sample tables (a few KB) stay in cache and are not counted.
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(golden_index: dict) -> dict | None:
-    """Time the reference's own pthread render_multi (oracle/_ref build) on this host
-    on a bounded sample of the same scene."""
-    entry = golden_index.get(CPU_SAMPLE_SCENE, {})
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks_if_needed(args) -> None:
+    """--gpus N without a torchrun environment: run N ranks under torchrun (a child process,
+    started before this process touches the GPU) and exit with its status."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+                   "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+            log("bench: starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+            sys.exit(subprocess.call(cmd))
+        return
+    if int(env_world) != args.gpus:
+        log("bench: --gpus %d but WORLD_SIZE=%s: refusing to measure a different GPU count" % (args.gpus, env_world))
+        sys.exit(2)
+
+
+def reference_rays(name: str):
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f).get(name, {}).get("reference_rays", {}).get("total")
+
+
+def cpu_baseline() -> dict | None:
+    """The reference's own pthread render_multi on this host, on a bounded sample of the workload:
+    the same camera and scene at 240x135 (1/64 of the pixels, 8x8 CMJ), CPU_SAMPLE_THREADS threads.
+    The binary is oracle/_ref/bin/<sample>: built from the reference's sources by oracle/build_ref.sh
+    in the build container (a git-ignored artefact that travels with the working tree; no reference
+    source is in the repo). Without it, the repository's own C restatement (oracle/, "port") is timed."""
+    rays = reference_rays(CPU_SAMPLE_SCENE)
     exe = os.path.join(ROOT, "oracle", "_ref", "bin", CPU_SAMPLE_SCENE)
-    rays = entry.get("reference_rays", {}).get("total")
-    if not os.path.exists(exe) or not rays:
-        log("cpu_baseline: reference sample binary or its ray count missing; skipped")
-        return None
-    stats = "/tmp/frt_bench_ref_stats_%d.json" % os.getpid()
-    os.makedirs("/tmp/frt_golden/out", exist_ok=True)
+    host_cpus = os.cpu_count()
+    if os.path.exists(exe) and rays:
+        stats = "/tmp/frt_bench_ref_stats_%d.json" % os.getpid()
+        os.makedirs("/tmp/frt_golden/out", exist_ok=True)
+        t0 = time.time()
+        proc = subprocess.run([exe], cwd=ASSETS, env=dict(os.environ, FRT_REF_STATS=stats), stdout=subprocess.DEVNULL,
+                              stderr=subprocess.PIPE, text=True, timeout=600)
+        if proc.returncode != 0:
+            log("cpu_baseline: reference run failed:", proc.stderr[-500:])
+            return None
+        st = json.load(open(stats))
+        secs = st["render_multi_seconds"]
+        return {"value": round(rays / secs / 1e6, 4), "unit": "Mrays/s", "cores": int(st["threads"]),
+                "kind": "reference", "threads": int(st["threads"]), "host_cpus_visible": host_cpus,
+                "seconds": round(secs, 3), "wall_seconds": round(time.time() - t0, 3),
+                "sample": "%s: the reference's render_multi (pthread pool, %d threads) built from /root/reference "
+                          "sources by oracle/build_ref.sh, %dx%dx%d spp (the benchmark camera at 1/64 of the "
+                          "pixels), %d reference rays counted by the oracle"
+                          % (CPU_SAMPLE_SCENE, st["threads"], st["width"], st["height"], st["usteps"] * st["vsteps"],
+                             rays)}
+    # checker leg only (never the GPU path): the oracle restatement on the same sample
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    from conftest import load_scene
+    scene = load_scene(CPU_SAMPLE_SCENE)
     t0 = time.time()
-    proc = subprocess.run([exe], cwd=ASSETS, env=dict(os.environ, FRT_REF_STATS=stats), stdout=subprocess.DEVNULL,
-                          stderr=subprocess.PIPE, text=True, timeout=600)
-    if proc.returncode != 0:
-        log("cpu_baseline: reference run failed:", proc.stderr[-500:])
-        return None
-    st = json.load(open(stats))
-    secs = st["render_multi_seconds"]
-    return {"value": round(rays / secs / 1e6, 4), "unit": "Mrays/s", "cores": int(st["threads"]),
-            "kind": "reference", "seconds": round(secs, 3), "wall_seconds": round(time.time() - t0, 3),
-            "sample": "%s: reference render_multi (pthread pool, %d threads), %dx%dx%d spp, %d reference rays"
-                      % (CPU_SAMPLE_SCENE, st["threads"], st["width"], st["height"], st["usteps"] * st["vsteps"], rays)}
+    _, st = oracle.render(scene, threads=CPU_SAMPLE_THREADS, stats=True)
+    secs = time.time() - t0
+    total = int(st["primary_rays"] + st["secondary_rays"] + st["shadow_rays"])
+    return {"value": round(total / secs / 1e6, 4), "unit": "Mrays/s", "cores": CPU_SAMPLE_THREADS, "kind": "port",
+            "threads": CPU_SAMPLE_THREADS, "host_cpus_visible": host_cpus, "seconds": round(secs, 3),
+            "sample": "%s: oracle/ C restatement of the reference (reference build absent), %d threads, %d rays"
+                      % (CPU_SAMPLE_SCENE, CPU_SAMPLE_THREADS, total)}
+
+
+def latest_pmc(kernel: str, workload: str):
+    """The newest committed PMC summary (profiles/rNN_pmc_*.json) of this kernel on this workload."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json"))):
+        try:
+            t = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if t.get("kernel") == kernel and t.get("workload") == workload:
+            best = (p, t)
+    return best
+
+
+def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> dict:
+    kname = "frt_jit_shadow" if d.get("shadow_jit") else "k_shadow"
+    avg_ms = kernel_ms["shadow"] / max(1, launches["shadow"])
+    per_launch = d["shadow_kernel_bytes"] / max(1, launches["shadow"])
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kname,
+            "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": launches["shadow"],
+            "algorithmic_bytes_per_launch": round(per_launch),
+            "timing": "HIP events around each launch on the engine stream (frt_frame_stats.kernel_ms)"}
+    found = latest_pmc(kname, workload)
+    if found:
+        path, t = found
+        roof["traffic"] = round(t["traffic_bytes_per_launch"])
+        roof["traffic_source"] = os.path.relpath(path, ROOT)
+        if "rocprof_avg_ms" in t:
+            roof["rocprof_avg_launch_ms"] = round(t["rocprof_avg_ms"], 4)
+        if "SQ_INSTS_VALU_per_launch" in t:
+            ginst = t["SQ_INSTS_VALU_per_launch"] / (avg_ms * 1e-3) / 1e9
+            roof["valu"] = {"achieved": round(ginst, 1), "peak": VALU_PEAK_GINST_S, "unit": "G wave64 VALU inst/s",
+                            "frac": round(ginst / VALU_PEAK_GINST_S, 3),
+                            "valu_inst_per_64_rays": round(t.get("valu_insts_per_wave", 0), 1)}
+    return roof
 
 
 def main():
@@ -83,66 +184,87 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--gi-steps", type=int, default=1, help="timed GI frames (0: skip the GI line)")
     ap.add_argument("--scene", default=DEFAULT_SCENE)
     ap.add_argument("--batch-samples", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-render-multi", action="store_true", help="skip the drop-in entry point timing")
     args = ap.parse_args()
+    launch_ranks_if_needed(args)
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
 
     from fast_ray_tracer_amd import build
     from fast_ray_tracer_amd.dist import gather_canvas, shard_capacity
-    from fast_ray_tracer_amd.runtime import GpuRenderer, Scene
+    from fast_ray_tracer_amd.runtime import GpuRenderer, Scene, render_multi
 
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    main_c = os.path.join(GOLDEN, "scenes", args.scene + ".c")
-    scene_so = os.path.join(build.SCENE_LIB, args.scene + ".so")
-    if rank == 0 and not os.path.exists(scene_so):
-        build.build_scene(main_c)
-    if world > 1:
-        dist.barrier()
+    def scene_of(name):
+        so = os.path.join(build.SCENE_LIB, name + ".so")
+        if rank == 0 and not os.path.exists(so):
+            build.build_scene(os.path.join(GOLDEN, "scenes", name + ".c"))
+        if world > 1:
+            dist.barrier()
+        return Scene(so, asset_root=ASSETS)
 
-    scene = Scene(scene_so, asset_root=ASSETS)
-    renderer = GpuRenderer(scene, device=local_rank)
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    scene = scene_of(args.scene)
     H, W = scene.height, scene.width
+
+    # the drop-in entry point, once cold (includes the hiprtc compile of the scene's shadow kernel) and
+    # once warm, on device 0 only (rank 0 of a 1-rank run; outside the timed region)
+    rm = {}
+    if world == 1 and not args.no_render_multi:
+        torch.cuda.init()
+        for key in ("render_multi_wall_ms", "render_multi_wall_ms_warm"):
+            t0 = time.perf_counter()
+            render_multi(scene, devices=str(local_rank))
+            rm[key] = round(1e3 * (time.perf_counter() - t0), 2)
+        ndev = torch.cuda.device_count()
+        if ndev > 1:  # the in-process multi-GPU path of render_multi (one host thread per device)
+            t0 = time.perf_counter()
+            render_multi(scene, devices=",".join(str(i) for i in range(ndev)))
+            rm["render_multi_all_devices_wall_ms"] = round(1e3 * (time.perf_counter() - t0), 2)
+            rm["render_multi_all_devices"] = ndev
+
+    renderer = GpuRenderer(scene, device=local_rank)
     cap = shard_capacity(world, H)
     shard = torch.zeros((cap, W, 4), dtype=torch.float64, device="cuda")
 
-    def frame(stats=False):
-        st = renderer.render_into(shard.data_ptr(), row_begin=rank, row_end=H, row_stride=world,
-                                  batch_samples=args.batch_samples, stats=stats)
-        canvas = gather_canvas(shard, rank, world, H)
+    def frame(r, sh, height, seed=0x5EED, stats=False):
+        st = r.render_into(sh.data_ptr(), row_begin=rank, row_end=height, row_stride=world,
+                           batch_samples=args.batch_samples, seed=seed, stats=stats)
+        canvas = gather_canvas(sh, rank, world, height)
         return st, canvas
 
     for _ in range(args.warmup):
-        frame()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+        frame(renderer, shard, H)
+    sync()
 
     # timed region: exactly K frames, without per-kernel instrumentation (the engine still checks its
     # error flags every frame and fails the render if one is set)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        frame(stats=False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+        frame(renderer, shard, H)
+    sync()
     elapsed = time.perf_counter() - t0
 
     # one instrumented frame after the timed region: per-kernel HIP-event times on the engine stream and
     # the rays traced per frame (the same every frame: same scene, same seed)
-    st, _ = frame(stats=True)
+    st, _ = frame(renderer, shard, H, stats=True)
     d = st.as_dict()
     if d["errors"]:
         raise RuntimeError("engine reported errors: %s" % d)
@@ -157,43 +279,59 @@ def main():
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
     t_max = float(t.item())
     total_rays = float(rays.item())
-    last = d
+    renderer.close()
+    del shard
+
+    # ---- GI (configs[4]): fresh photon maps inside every timed frame ----
+    gi = None
+    if args.gi_steps > 0:
+        gscene = scene_of(GI_SCENE)
+        gr = GpuRenderer(gscene, device=local_rank)
+        gshard = torch.zeros((shard_capacity(world, gscene.height), gscene.width, 4), dtype=torch.float64, device="cuda")
+        sync()
+        g0 = time.perf_counter()
+        gstats = []
+        for i in range(args.gi_steps):
+            # a new seed per frame: the engine traces new photon maps (frt_frame_stats.photon_pass)
+            gst, _ = frame(gr, gshard, gscene.height, seed=0x61000 + i, stats=True)
+            gstats.append(gst.as_dict())
+        sync()
+        g_elapsed = time.perf_counter() - g0
+        gd = gstats[-1]
+        if any(s["errors"] for s in gstats):
+            raise RuntimeError("engine reported errors in the GI frame: %s" % gstats)
+        g_rays = sum(s["primary_rays"] + s["secondary_rays"] + s["shadow_rays"] + s["gather_rays"] for s in gstats)
+        gt = torch.tensor([g_elapsed], dtype=torch.float64, device="cuda")
+        gr_t = torch.tensor([float(g_rays)], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+            dist.all_reduce(gr_t, op=dist.ReduceOp.SUM)
+        gi = {"workload": GI_SCENE, "width": gscene.width, "height": gscene.height, "spp": gscene.spp,
+              "steps": args.gi_steps, "ms_per_step": round(1e3 * float(gt.item()) / args.gi_steps, 2),
+              "value": round(float(gr_t.item()) / float(gt.item()) / 1e6, 3),
+              "unit": "Mrays/s (primary+secondary+shadow+final-gather)",
+              "photon_pass_in_timed_region": all(s["photon_pass"] for s in gstats),
+              "photon_ms": round(gd["photon_ms"], 2), "photons": gd["photons"],
+              "gather_rays_per_frame": gd["gather_rays"],
+              "kernel_ms_per_frame": {k: round(v, 3) for k, v in gd["kernel_ms"].items()},
+              "data": "reference codegen main.c of scenes/cornell_box as shipped (GI on, 65535-row light cache, "
+                      "jitter off) with the camera at 1920x1080x64; statistical parity (tests/test_gpu_stochastic.py)"}
+        if gd.get("gather_est_ms"):
+            gi["gather_est"] = {"ms_per_frame": round(gd["gather_est_ms"], 3),
+                                "launches": gd.get("gather_est_launches")}
+        gr.close()
 
     if rank == 0:
-        with open(os.path.join(GOLDEN, "golden.json")) as f:
-            gidx = json.load(f)
         ms_per_step = 1e3 * t_max / args.steps
         value = total_rays / t_max / 1e6
-        ref_rays = gidx.get(args.scene, {}).get("reference_rays", {}).get("total")
-        # dominant kernel: the largest event time of the instrumented frame
+        ref_rays = reference_rays(args.scene)
         dom = max(kernel_ms, key=kernel_ms.get)
-        avg_ms = kernel_ms[dom] / max(1, launches[dom])
-        roof = None
         if dom == "shadow":
-            kname = "frt_jit_shadow" if last.get("shadow_jit") else "k_shadow"
-            bytes_per_frame = last["shadow_kernel_bytes"]  # engine-side byte model (see above)
-            per_launch = bytes_per_frame / max(1, launches[dom])
-            achieved = per_launch / (avg_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kname,
-                    "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": round(per_launch)}
-            # HBM bytes and VALU instructions per launch from the committed PMC passes of this kernel
-            # on this workload (tools/profile_round.sh); the kernel is VALU-issue bound, not HBM bound:
-            # "valu" relates its instruction count to the live kernel time
-            pmc = os.path.join(ROOT, "profiles", PMC_FILE)
-            if os.path.exists(pmc):
-                t = json.load(open(pmc))
-                if t.get("kernel") == kname and t.get("workload") == args.scene:
-                    roof["traffic"] = round(t["traffic_bytes_per_launch"])
-                    roof["traffic_source"] = "profiles/" + PMC_FILE
-                    if "SQ_INSTS_VALU_per_launch" in t:
-                        ginst = t["SQ_INSTS_VALU_per_launch"] / (avg_ms * 1e-3) / 1e9
-                        roof["valu"] = {"achieved": round(ginst, 1), "peak": VALU_PEAK_GINST_S,
-                                        "unit": "G wave64 VALU inst/s", "frac": round(ginst / VALU_PEAK_GINST_S, 3),
-                                        "valu_inst_per_64_rays": round(t.get("valu_insts_per_wave", 0), 1)}
+            roof = shadow_roofline(d, kernel_ms, launches, args.scene)
         else:
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                    "traffic": None, "kernel": dom, "avg_launch_ms": round(avg_ms, 4)}
+                    "traffic": None, "kernel": dom,
+                    "avg_launch_ms": round(kernel_ms[dom] / max(1, launches[dom]), 4)}
         out = {
             "metric": "Mrays/s (primary+shadow+secondary) + wall-clock/frame, 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -206,8 +344,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": ("reference codegen main.c of scenes/cornell_box (GI off, 1-row light cache)"
-                     if args.scene == DEFAULT_SCENE else "reference codegen main.c: tests/golden/scenes/%s.c" % args.scene),
+            "data": ("reference codegen main.c of scenes/cornell_box (GI off, 1-row light cache) at 1920x1080, "
+                     "8x8 CMJ" if args.scene == DEFAULT_SCENE
+                     else "reference codegen main.c: tests/golden/scenes/%s.c" % args.scene),
             "config": {"workload": args.scene, "width": W, "height": H, "spp": scene.spp,
                        "path_length": 5, "parallelism": "rows%d" % world},
             "rays_per_frame_traced": total_rays / args.steps,
@@ -216,10 +355,12 @@ def main():
             "kernel_ms_per_frame": {k: round(v, 4) for k, v in kernel_ms.items()},
             "roofline": roof,
         }
+        out.update(rm)
+        if gi is not None:
+            out["gi"] = gi
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(gidx)
+            out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
-    renderer.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

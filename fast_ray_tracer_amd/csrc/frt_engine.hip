@@ -44,6 +44,7 @@
 namespace frt {
 
 constexpr int kBlock = 256;
+constexpr int kMaxPathLength = 11;  // 12-bit heap code of a path node in its key (k_prepare)
 
 // path-node record of one level; node i of level d belongs to queued ray i
 struct NodeRec {
@@ -1464,6 +1465,15 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     S.cam = sc->camera;
     S.cfg = sc->config;
     h->host_lights.assign(sc->lights, sc->lights + sc->num_lights);
+    // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
+    // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L
+    // has codes up to 2^(L+1) - 1, so L <= 11. The reference accepts any length; deeper recursion
+    // is refused here with the reason rather than rendered with colliding keys.
+    if (S.cfg.path_length < 0 || S.cfg.path_length > frt::kMaxPathLength) {
+        frt_scene_release(h);
+        return fail("frt_scene_upload: path-length " + std::to_string(S.cfg.path_length) +
+                    " is not supported (0.." + std::to_string(frt::kMaxPathLength) + ")");
+    }
     if (S.cfg.use_gi && (S.cfg.gi_path_length >= 255 || S.cfg.photon_count <= 0)) {
         frt_scene_release(h);
         return fail("frt_scene_upload: global illumination needs photon maps (photon_count > 0) and path_length < 255");
@@ -1671,8 +1681,18 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
         void* args[] = {&h->S, (void*)&B, (void*)&rec, &n, &h->j_light, &h->j_point, &h->samples_per_node,
                         &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
-        hip_ignore(hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(work, frt::kTraceBlock), 1, 1,
-                                         frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr));
+        const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(work, frt::kTraceBlock), 1, 1,
+                                                    frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
+        if (le != hipSuccess) {
+            // the counts are still the zero memset: run the generic walk for this launch and the rest of
+            // the handle's life instead of rendering everything shadowed
+            std::fprintf(stderr, "frt: scene-specialised shadow kernel launch failed (%s); generic walk\n",
+                         hipGetErrorString(le));
+            (void)hipGetLastError();
+            h->jit_shadow = nullptr;
+            launch_shadow(h, B, rec, n, counts);
+            return;
+        }
         switch (h->S.features & 3) {
         case 0: launch_shadow_redo_f<0>(h, B, rec, n, counts); break;
         case 1: launch_shadow_redo_f<1>(h, B, rec, n, counts); break;
@@ -2037,7 +2057,17 @@ static void dump_walk_stats(frt_scene_handle* h) {
 }
 #endif
 
+static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st);
+
+// a failed frame leaves no half-built state behind: photon maps traced by it (maybe truncated by a
+// store overflow) are not reused by the next frame with the same seed
 static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
+    const int rc = render_frame(h, P, dev_out, st);
+    if (rc) h->gi.built = false;
+    return rc;
+}
+
+static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
     using namespace frt;
     FRT_HIP(hipSetDevice(h->device));
     const int64_t hs = h->S.cam.hsize;
@@ -2071,6 +2101,7 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
             float ms = 0.f;
             hip_ignore(hipEventElapsedTime(&ms, p0, p1));
             st->photon_ms = ms;
+            st->photon_pass = 1;
             hip_ignore(hipEventDestroy(p0));
             hip_ignore(hipEventDestroy(p1));
         }

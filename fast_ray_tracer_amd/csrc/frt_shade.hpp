@@ -16,8 +16,9 @@ __device__ __forceinline__ int first_xf(const DevScene& S, int leaf) {
     return S.nodes[leaf].xform >= 0 ? leaf : S.nodes[leaf].tparent;
 }
 
-// shape_world_to_object (shapes.c:117-131): root-most transform first
-__device__ inline void world_to_object(const DevScene& S, int leaf, const double* p, double* out) {
+// shape_world_to_object (shapes.c:117-131): root-most transform first; w0: the point's w is 0
+// (a perturbed pattern's point, see pattern_at_shape), so no transform adds its translation
+__device__ inline void world_to_object(const DevScene& S, int leaf, const double* p, double* out, bool w0 = false) {
     double q[3] = {p[0], p[1], p[2]};
     const int first = first_xf(S, leaf);
     int n = 0;
@@ -26,7 +27,8 @@ __device__ inline void world_to_object(const DevScene& S, int leaf, const double
         int x = first;
         for (int j = 0; j < k; ++j) x = S.nodes[x].tparent;
         double t[3];
-        xf_point(xform_of(S, S.nodes[x].xform), q, t);
+        if (w0) xf_vector(xform_of(S, S.nodes[x].xform), q, t);
+        else xf_point(xform_of(S, S.nodes[x].xform), q, t);
         q[0] = t[0];
         q[1] = t[1];
         q[2] = t[2];
@@ -367,26 +369,26 @@ __device__ inline double pnoise3(double x, double y, double z, double persistenc
     return total;
 }
 
-// pattern_at_shape for world point wp (pattern.c:10-116)
+// pattern_at_shape for world point wp (pattern.c:10-116); w0: wp's w component is 0 (below)
 template <int D>
 __device__ void pattern_at_shape(const DevScene& S, int pi, int leaf, const double* wp, double* out,
-                                 const double* ov_a = nullptr, const double* ov_b = nullptr) {
+                                 const double* ov_a = nullptr, const double* ov_b = nullptr, bool w0 = false) {
     const frt_pattern& P = S.patterns[pi];
     if constexpr (D > 0) {
         if (P.type == 10) {  // BLENDED
             double c1[3], c2[3];
-            pattern_at_shape<D - 1>(S, P.child[0], leaf, wp, c1);
-            pattern_at_shape<D - 1>(S, P.child[1], leaf, wp, c2);
+            pattern_at_shape<D - 1>(S, P.child[0], leaf, wp, c1, nullptr, nullptr, w0);
+            pattern_at_shape<D - 1>(S, P.child[1], leaf, wp, c2, nullptr, nullptr, w0);
             for (int k = 0; k < 3; ++k) out[k] = (c1[k] + c2[k]) / 2.0;
             return;
         }
         if (P.type == 11) {  // NESTED
             double c1[3], c2[3];
-            pattern_at_shape<D - 1>(S, P.child[1], leaf, wp, c1);
-            pattern_at_shape<D - 1>(S, P.child[2], leaf, wp, c2);
+            pattern_at_shape<D - 1>(S, P.child[1], leaf, wp, c1, nullptr, nullptr, w0);
+            pattern_at_shape<D - 1>(S, P.child[2], leaf, wp, c2, nullptr, nullptr, w0);
             const frt_pattern& prim = S.patterns[P.child[0]];
-            if (prim.type <= 4) pattern_at_shape<D - 1>(S, P.child[0], leaf, wp, out, c1, c2);
-            else pattern_at_shape<D - 1>(S, P.child[0], leaf, wp, out);
+            if (prim.type <= 4) pattern_at_shape<D - 1>(S, P.child[0], leaf, wp, out, c1, c2, w0);
+            else pattern_at_shape<D - 1>(S, P.child[0], leaf, wp, out, nullptr, nullptr, w0);
             return;
         }
         if (P.type == 12) {  // PERTURBED
@@ -399,13 +401,17 @@ __device__ void pattern_at_shape(const DevScene& S, int pi, int leaf, const doub
             if (z < 0) z -= 1.0;
             else z += 1.0;
             q[2] = wp[2] + P.scale_factor * pnoise3(x, y, z, P.persistence, P.frequency, P.octaves, P.seed);
-            pattern_at_shape<D - 1>(S, P.child[0], leaf, q, out);
+            // the reference leaves the perturbed point's w uninitialised (pattern.c:110-113) and its
+            // build reads it as 0 (pinned by the patterns_160x80 golden): the object and pattern
+            // transforms then apply without their translations
+            pattern_at_shape<D - 1>(S, P.child[0], leaf, q, out, nullptr, nullptr, true);
             return;
         }
     }
     double op[3], pp[3];
-    world_to_object(S, leaf, wp, op);
+    world_to_object(S, leaf, wp, op, w0);
     if (P.transform_identity) copy3(op, pp);
+    else if (w0) xf_vector(P.inv, op, pp);
     else xf_point(P.inv, op, pp);
     base_pattern_at(S, P, leaf, pp, ov_a ? ov_a : P.color[0], ov_b ? ov_b : P.color[1], out);
 }

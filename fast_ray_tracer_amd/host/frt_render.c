@@ -7,10 +7,12 @@
  * writes and frees. Instead of a pthread pool over deep world copies, the
  * scene is flattened once (frt_flatten.c) and rendered on an MI355X through
  * the device C ABI (include/frt_device.h). There is no CPU fallback: if the
- * device path cannot run, the process stops with a message.
+ * device path cannot run, render_multi logs the reason and returns a zeroed
+ * canvas (the reference has no error return).
  *
  * Environment knobs (main.c stays unchanged):
- *   FRT_DEVICE=<n>         HIP device to render on (default 0)
+ *   FRT_DEVICES=<i,j,..>   devices to split the rows over (default: every visible GPU)
+ *   FRT_GPUS=<n>           devices 0..n-1;  FRT_DEVICE=<n>: that one device
  *   FRT_SEED=<u64>         counter-RNG seed for multi-row area-light caches
  *   FRT_STATS_OUT=<file>   write a JSON line of frame statistics
  *
@@ -19,6 +21,7 @@
  * Camera / World without rendering (used by the Python bindings, tests and
  * bench.py).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -51,19 +54,29 @@ unsupported_config(World w, Camera cam, char *err, size_t n)
     return 0;
 }
 
-frt_scene_handle *
-frt_host_prepare(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter, int device)
+/* flatten + check: the device-independent half of frt_host_prepare */
+static int
+host_flatten(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter, frt_scene *fs)
 {
     g_host_error[0] = '\0';
     if (w == NULL || cam == NULL || w->global_config == NULL) {
         snprintf(g_host_error, sizeof(g_host_error), "null camera / world / global_config");
-        return NULL;
+        return -1;
     }
     if (unsupported_config(w, cam, g_host_error, sizeof(g_host_error))) {
-        return NULL;
+        return -1;
     }
+    if (frt_flatten_scene(cam, w, usteps, vsteps, jitter, fs, g_host_error, sizeof(g_host_error))) {
+        return -1;
+    }
+    return 0;
+}
+
+frt_scene_handle *
+frt_host_prepare(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter, int device)
+{
     frt_scene fs;
-    if (frt_flatten_scene(cam, w, usteps, vsteps, jitter, &fs, g_host_error, sizeof(g_host_error))) {
+    if (host_flatten(cam, w, usteps, vsteps, jitter, &fs)) {
         return NULL;
     }
     frt_scene_handle *h = NULL;
@@ -77,50 +90,224 @@ frt_host_prepare(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter,
 }
 
 static void
-write_stats(const char *path, const frt_frame_stats *st, Camera cam, size_t usteps, size_t vsteps)
+write_stats(const char *path, const frt_frame_stats *st, Camera cam, size_t usteps, size_t vsteps, int ndev)
 {
     FILE *f = fopen(path, "w");
     if (f == NULL) {
         return;
     }
     fprintf(f,
-            "{\"width\": %zu, \"height\": %zu, \"usteps\": %zu, \"vsteps\": %zu, \"render_ms\": %.6f, "
+            "{\"width\": %zu, \"height\": %zu, \"usteps\": %zu, \"vsteps\": %zu, \"devices\": %d, \"render_ms\": %.6f, "
             "\"primary_rays\": %llu, \"secondary_rays\": %llu, \"shadow_rays\": %llu, "
             "\"pruned_secondary\": %llu, \"errors\": %llu}\n",
-            cam->hsize, cam->vsize, usteps, vsteps, st->render_ms, (unsigned long long)st->primary_rays,
+            cam->hsize, cam->vsize, usteps, vsteps, ndev, st->render_ms, (unsigned long long)st->primary_rays,
             (unsigned long long)st->secondary_rays, (unsigned long long)st->shadow_rays,
             (unsigned long long)st->pruned_secondary, (unsigned long long)st->errors);
     fclose(f);
 }
 
+/*
+ * Devices render_multi uses, in order:
+ *   FRT_DEVICES=<i,j,...>  explicit list (a device may repeat: several handles on one GPU)
+ *   FRT_GPUS=<n>           devices 0 .. n-1
+ *   otherwise              every visible device (the reference's pool is sized by
+ *                          threading.num_threads; here the unit of parallelism is a GPU)
+ * FRT_DEVICE=<n> (round 1) selects one device.
+ */
+#define FRT_MAX_RENDER_DEVICES 64
+
+static int
+render_devices(int *dev, int cap, char *err, size_t errlen)
+{
+    const int visible = frt_device_count();
+    int n = 0;
+    const char *list = getenv("FRT_DEVICES");
+    const char *count = getenv("FRT_GPUS");
+    const char *one = getenv("FRT_DEVICE");
+    if (list != NULL && *list) {
+        const char *q = list;
+        while (*q && n < cap) {
+            char *end = NULL;
+            long v = strtol(q, &end, 10);
+            if (end == q) {
+                break;
+            }
+            dev[n++] = (int)v;
+            q = (*end == ',') ? end + 1 : end;
+        }
+    } else if (count != NULL && *count) {
+        int k = atoi(count);
+        for (int i = 0; i < k && n < cap; ++i) {
+            dev[n++] = i;
+        }
+    } else if (one != NULL && *one) {
+        dev[n++] = atoi(one);
+    } else {
+        for (int i = 0; i < visible && n < cap; ++i) {
+            dev[n++] = i;
+        }
+    }
+    if (visible <= 0) {
+        snprintf(err, errlen, "no HIP device visible (the GPU path has no CPU fallback)");
+        return -1;
+    }
+    if (n == 0) {
+        snprintf(err, errlen, "no render device selected (FRT_DEVICES / FRT_GPUS)");
+        return -1;
+    }
+    for (int i = 0; i < n; ++i) {
+        if (dev[i] < 0 || dev[i] >= visible) {
+            snprintf(err, errlen, "render device %d out of range (%d visible)", dev[i], visible);
+            return -1;
+        }
+    }
+    return n;
+}
+
+/* one device's share of the frame: upload, render rows k, k+N, k+2N, ..., release */
+typedef struct {
+    const frt_scene *fs;
+    int device, k, n;
+    int64_t height, width;
+    uint64_t seed;
+    double *rows;             /* rows_of(k) x width x 4 */
+    int want_stats;
+    frt_frame_stats st;
+    int rc;
+    char err[512];
+} device_job;
+
+static void *
+device_worker(void *arg)
+{
+    device_job *j = (device_job *)arg;
+    frt_scene_handle *h = NULL;
+    j->rc = frt_scene_upload(j->fs, j->device, &h);
+    if (j->rc) {
+        snprintf(j->err, sizeof(j->err), "device %d: upload: %s", j->device, frt_last_error());
+        return NULL;
+    }
+    frt_frame_params p;
+    memset(&p, 0, sizeof(p));
+    p.row_begin = j->k;
+    p.row_end = j->height;
+    p.row_stride = j->n;
+    p.seed = j->seed;
+    j->rc = frt_render_rows(h, &p, j->rows, j->want_stats ? &j->st : NULL);
+    if (j->rc) {
+        snprintf(j->err, sizeof(j->err), "device %d: render: %s", j->device, frt_last_error());
+    }
+    frt_scene_release(h);
+    return NULL;
+}
+
+/*
+ * The drop-in entry point (reference renderer.c:244-281). Rows are interleaved
+ * over the selected devices (row r on device r mod N), each device rendering
+ * from its own copy of the flattened scene on its own host thread and stream;
+ * the rows are then placed into the caller's canvas — a placement, not a
+ * reduction, so the canvas is bit-identical for any device count. The
+ * reference has no error return: on failure this logs the reason to stderr
+ * and returns the (zeroed) canvas, as SURVEY.md 8(b) asks of a replacement.
+ */
 Canvas
 render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
 {
-    const char *dev_env = getenv("FRT_DEVICE");
-    int device = dev_env ? atoi(dev_env) : 0;
-    frt_scene_handle *h = frt_host_prepare(cam, w, usteps, vsteps, jitter, device);
-    if (h == NULL) {
+    const size_t width = cam != NULL ? cam->hsize : 1, height = cam != NULL ? cam->vsize : 1;
+    Canvas c = canvas_alloc(width, height, false, NULL);
+    memset(c->arr, 0, width * height * sizeof(Color));
+    int dev[FRT_MAX_RENDER_DEVICES];
+    char err[512];
+    frt_scene fs;
+    if (host_flatten(cam, w, usteps, vsteps, jitter, &fs)) {
         fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", g_host_error);
-        exit(2);
+        return c;
     }
-    Canvas c = canvas_alloc(cam->hsize, cam->vsize, false, NULL);
-    frt_frame_params p;
-    memset(&p, 0, sizeof(p));
-    p.row_begin = 0;
-    p.row_end = (int64_t)cam->vsize;
-    p.row_stride = 1;
+    const int n = render_devices(dev, FRT_MAX_RENDER_DEVICES, err, sizeof(err));
+    if (n < 0) {
+        fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", err);
+        frt_flat_scene_free(&fs);
+        return c;
+    }
     const char *seed_env = getenv("FRT_SEED");
-    p.seed = seed_env ? strtoull(seed_env, NULL, 10) : 0x5eedULL;
-    frt_frame_stats st;
+    const uint64_t seed = seed_env ? strtoull(seed_env, NULL, 10) : 0x5eedULL;
     const char *stats_path = getenv("FRT_STATS_OUT");
-    if (frt_render_rows(h, &p, (double *)c->arr, stats_path ? &st : NULL)) {
-        fprintf(stderr, "frt: render failed: %s\n", frt_last_error());
-        exit(3);
+    device_job *jobs = (device_job *)calloc((size_t)n, sizeof(device_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)n, sizeof(pthread_t));
+    int failed = jobs == NULL || th == NULL;
+    for (int k = 0; !failed && k < n; ++k) {
+        device_job *j = &jobs[k];
+        const int64_t nrows = ((int64_t)height - k + n - 1) / n;
+        j->fs = &fs;
+        j->device = dev[k];
+        j->k = k;
+        j->n = n;
+        j->height = (int64_t)height;
+        j->width = (int64_t)width;
+        j->seed = seed;
+        j->want_stats = stats_path != NULL;
+        j->rows = (double *)malloc((size_t)(nrows > 0 ? nrows : 1) * width * 4 * sizeof(double));
+        if (j->rows == NULL) {
+            failed = 1;
+            snprintf(err, sizeof(err), "out of host memory");
+        }
     }
-    if (stats_path) {
-        write_stats(stats_path, &st, cam, usteps, vsteps);
+    int started = 0;
+    if (!failed) {
+        if (n == 1) {
+            device_worker(&jobs[0]);  /* no extra thread for the common single-device case */
+            started = 0;
+        } else {
+            for (; started < n; ++started) {
+                if (pthread_create(&th[started], NULL, device_worker, &jobs[started])) {
+                    break;
+                }
+            }
+            for (int k = 0; k < started; ++k) {
+                pthread_join(th[k], NULL);
+            }
+            if (started < n) {
+                failed = 1;
+                snprintf(err, sizeof(err), "pthread_create failed");
+            }
+        }
     }
-    frt_scene_release(h);
+    frt_frame_stats total;
+    memset(&total, 0, sizeof(total));
+    for (int k = 0; !failed && k < n; ++k) {
+        if (jobs[k].rc) {
+            failed = 1;
+            snprintf(err, sizeof(err), "%s", jobs[k].err);
+        }
+    }
+    if (!failed) {
+        for (int k = 0; k < n; ++k) {
+            const device_job *j = &jobs[k];
+            int64_t i = 0;
+            for (int64_t r = k; r < (int64_t)height; r += n, ++i) {
+                memcpy(c->arr + (size_t)r * width, j->rows + (size_t)i * width * 4, width * sizeof(Color));
+            }
+            total.primary_rays += j->st.primary_rays;
+            total.secondary_rays += j->st.secondary_rays;
+            total.shadow_rays += j->st.shadow_rays;
+            total.pruned_secondary += j->st.pruned_secondary;
+            total.errors |= j->st.errors;
+            if (j->st.render_ms > total.render_ms) {
+                total.render_ms = j->st.render_ms;
+            }
+        }
+        if (stats_path) {
+            write_stats(stats_path, &total, cam, usteps, vsteps, n);
+        }
+    } else {
+        fprintf(stderr, "frt: render_multi failed: %s\n", err);
+    }
+    for (int k = 0; jobs != NULL && k < n; ++k) {
+        free(jobs[k].rows);
+    }
+    free(jobs);
+    free(th);
+    frt_flat_scene_free(&fs);
     return c;
 }
 
@@ -195,6 +382,16 @@ size_t frt_captured_vsteps(void) { return g_capture.vsteps; }
 int frt_captured_jitter(void) { return g_capture.jitter ? 1 : 0; }
 void frt_captured_drand48(unsigned short out[3]) { memcpy(out, g_capture.drand48_state, sizeof(g_capture.drand48_state)); }
 void frt_set_drand48(const unsigned short in[3]) { seed48((unsigned short *)in); }
+double *frt_canvas_data(Canvas c) { return (double *)c->arr; }
+
+/* test hook: set the captured world's direct-illumination path length, returning the old one */
+int
+frt_world_path_length(World w, int v)
+{
+    const int old = (int)w->global_config->illumination.di.path_length;
+    w->global_config->illumination.di.path_length = (size_t)v;
+    return old;
+}
 size_t frt_camera_hsize(Camera c) { return c->hsize; }
 size_t frt_camera_vsize(Camera c) { return c->vsize; }
 

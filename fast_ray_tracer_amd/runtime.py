@@ -35,7 +35,7 @@ class FrameStats(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_uint64 * 8),
                 ("shadow_kernel_bytes", ctypes.c_double), ("gather_rays", ctypes.c_uint64),
                 ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double),
-                ("shadow_jit", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("shadow_jit", ctypes.c_int32), ("photon_pass", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
@@ -46,6 +46,7 @@ class FrameStats(ctypes.Structure):
             "shadow_kernel_bytes": float(self.shadow_kernel_bytes),
             "gather_rays": int(self.gather_rays), "photons": [int(self.photons[0]), int(self.photons[1])],
             "photon_ms": float(self.photon_ms), "shadow_jit": int(self.shadow_jit),
+            "photon_pass": int(self.photon_pass),
             "kernel_ms": {names[i]: float(self.kernel_ms[i]) for i in range(8) if self.kernel_launches[i]},
             "kernel_launches": {names[i]: int(self.kernel_launches[i]) for i in range(8) if self.kernel_launches[i]},
         }
@@ -185,6 +186,42 @@ class GpuRenderer:
         if rc != 0:
             raise RuntimeError("frt render failed: " + self.lib.frt_last_error().decode())
         return st if stats else None
+
+
+def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
+    """The drop-in entry point itself: ``render_multi(cam, world, usteps, vsteps, jitter)``
+    (host/frt_render.c; reference renderer.c:244) on the captured scene — flatten, upload
+    (incl. the scene-specialised kernel's compile), render over the selected devices
+    (``FRT_DEVICES`` list, e.g. "0,0"; default every visible GPU), copy to the host canvas.
+    Returns the (height, width, 4) canvas; render_multi's failures are logged by it and
+    leave the canvas zeroed, so a zero canvas here raises."""
+    lib = host_lib()
+    vp = ctypes.c_void_p
+    lib.render_multi.restype = vp
+    lib.render_multi.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool]
+    lib.canvas_free.argtypes = [vp]
+    old = os.environ.get("FRT_DEVICES")
+    if devices is not None:
+        os.environ["FRT_DEVICES"] = devices
+    try:
+        c = lib.render_multi(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter)
+    finally:
+        if devices is not None:
+            if old is None:
+                os.environ.pop("FRT_DEVICES", None)
+            else:
+                os.environ["FRT_DEVICES"] = old
+    try:
+        # struct canvas (canvas.h): size_t width, height; bool super_sample; ...; Color *arr — read via the helper
+        lib.frt_canvas_data.restype = ctypes.POINTER(ctypes.c_double)
+        lib.frt_canvas_data.argtypes = [vp]
+        ptr = lib.frt_canvas_data(c)
+        out = np.ctypeslib.as_array(ptr, shape=(scene.height, scene.width, 4)).copy()
+    finally:
+        lib.canvas_free(c)
+    if not out.any():
+        raise RuntimeError("frt: render_multi returned an empty canvas (see its stderr message)")
+    return out
 
 
 def jit_check(scene: Scene) -> tuple[int, str, str]:

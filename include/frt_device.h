@@ -215,7 +215,7 @@ typedef struct frt_frame_stats {
     uint64_t photons[2];          /* photons in the caustic / global map used by this frame */
     double photon_ms;             /* photon tracing + map build of this frame (0 when the maps were reused) */
     int32_t shadow_jit;           /* 1: the scene-specialised shadow kernel ran (frt_jit.hip), 0: the generic walk */
-    int32_t pad;
+    int32_t photon_pass;          /* 1: this frame traced its photon maps (a new seed), 0: maps reused / no GI */
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */

@@ -916,12 +916,15 @@ pattern_at_shape(Pattern p, Shape s, const double *pt, double *res)
         double c1[4], c2[4];
         pattern_at_shape(p->fields.nested.pattern2, s, pt, c1);
         pattern_at_shape(p->fields.nested.pattern3, s, pt, c2);
-        Pattern prim = p->fields.nested.pattern1;
-        if (prim->type <= STRIPE_PATTERN) {
-            memcpy(prim->fields.concrete.a, c1, sizeof(Color));
-            memcpy(prim->fields.concrete.b, c2, sizeof(Color));
+        /* the reference writes c1 / c2 into the shared primary pattern and then evaluates it (a data
+         * race between its render threads, "TODO not threadsafe"); single-threaded that is the primary
+         * evaluated with colors (c1, c2), which a private copy gives without the race */
+        struct pattern prim = *p->fields.nested.pattern1;
+        if (prim.type <= STRIPE_PATTERN) {
+            memcpy(prim.fields.concrete.a, c1, sizeof(Color));
+            memcpy(prim.fields.concrete.b, c2, sizeof(Color));
         }
-        pattern_at_shape(prim, s, pt, res);
+        pattern_at_shape(&prim, s, pt, res);
         return;
     }
     case PERTURBED_PATTERN: { /* pattern.c:80-116 */
@@ -935,7 +938,10 @@ pattern_at_shape(Pattern p, Shape s, const double *pt, double *res)
         if (z < 0) z -= 1.0;
         else z += 1.0;
         q[2] = pt[2] + f->scale_factor * pnoise3(x, y, z, f->persistence, f->frequency, (int)f->octaves, f->seed);
-        q[3] = pt[3];
+        /* the reference leaves the perturbed point's w uninitialised (pattern.c:110-113); its build reads it
+         * as 0.0 (pinned by the patterns_160x80 golden), which drops the translations of the
+         * object and pattern transforms applied to it */
+        q[3] = 0.0;
         pattern_at_shape(f->pattern1, s, q, res);
         return;
     }

@@ -105,7 +105,60 @@ SCENES = {
     "cornell_direct_200_4x4_t16": ("scenes/cornell_box/cornell_box.yml",
                                    {"size": (200, 200), "cache": 1, "gi_off": True, "threads": 16,
                                     "ref_binary_only": True}),
+    # ---- round 2 ----
+    # the north-star headline: cornell_box at 1920x1080 with an 8x8 CMJ grid (64 spp), deterministic
+    # parity variant (GI off, single-row light cache); bench.py's default workload. No canvas golden
+    # (the reference needs ~20 min at 16 threads): parity at full size is a row band vs the oracle
+    "cornell_direct_1920x1080_8x8": ("scenes/cornell_box/cornell_box.yml",
+                                     {"size": (1920, 1080), "steps": (8, 8), "cache": 1, "gi_off": True,
+                                      "no_golden": True}),
+    # the same camera at 1/64 of the pixels (same 16:9 view, 8x8 CMJ): a canvas golden of the headline
+    # configuration and bench.py's cpu_baseline sample (the reference's pthread pool, 16 threads)
+    "cornell_direct_240x135_8x8": ("scenes/cornell_box/cornell_box.yml",
+                                   {"size": (240, 135), "steps": (8, 8), "cache": 1, "gi_off": True,
+                                    "threads": 16}),
+    # BASELINE configs[4]: the shipped GI configuration (1M photons, 8x8 final gather) at 1920x1080x64
+    "cornell_gi_1920x1080_8x8": ("scenes/cornell_box/cornell_box.yml",
+                                 {"size": (1920, 1080), "steps": (8, 8), "no_golden": True}),
+    # cfg4 stand-in (bounding_boxes: 6 dragons, BVH) at its 4x4 CMJ grid, small frame
+    "bounding_boxes_100x125_4x4": ("scenes/bounding_boxes/bounding_boxes.yml",
+                                   {"size": (100, 125), "steps": (4, 4)}),
+    # sibenik.yml (cfg4) with the missing sibenik.obj replaced by the textured nave fixture
+    # (make_fixture_mesh.py): OBJ+MTL, map_Ka / map_Kd PNG textures through triangle_uv_map,
+    # map_bump, smooth (vn) and flat triangles
+    "nave_120x150_4x4": ("scenes/sibenik/sibenik.yml",
+                         {"size": (120, 150), "steps": (4, 4), "gi_off": True,
+                          "define": {"sibenik": {"file": "scenes/frt_nave/nave.obj", "transform": []}},
+                          "camera": {"from": [0, 1.7, -3.6], "to": [0, 1.3, 4], "field-of-view": 1.3},
+                          "extra_assets": ["scenes/frt_nave/nave.obj", "scenes/frt_nave/nave.mtl",
+                                           "scenes/sibenik/mramor6x6.png", "scenes/sibenik/mramor6x6-bump.png",
+                                           "scenes/sibenik/KAMEN-stup.png", "scenes/sibenik/kamen.png"]}),
+    # (cornell_box_water.yml is not covered: the reference build segfaults while loading
+    # CornellBox-Water.obj, so there is nothing to compare against)
+    # frt fixture scenes (tests/golden/yml): branches no shipped scene enables
+    # (one reference thread: nested_pattern_at_shape writes into the shared primary pattern, a race
+    # between the reference's render threads that makes its multi-threaded image irreproducible)
+    "patterns_160x80": ("frt:patterns_160x80.yml", {"threads": 1}),
+    "circle_light_100": ("frt:circle_light_100.yml", {}),
+    "hemisphere_light_100": ("frt:hemisphere_light_100.yml", {}),
+    # the other apertures of camera.c:12-82 (dof.yml:14-19), statistical (drand48 in the reference)
+    "checkered_sphere_dof_cross_100": ("scenes/checkered_sphere/checkered_sphere.yml",
+                                       {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
+                                        "aperture": (["CROSS_APERTURE", -0.1, 0.1, -0.1, 0.1], 0.4),
+                                        "extra_seeds": STOCHASTIC_SEEDS}),
+    "checkered_sphere_dof_diamond_100": ("scenes/checkered_sphere/checkered_sphere.yml",
+                                         {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
+                                          "aperture": (["DIAMOND_APERTURE", -1, 1, -1, 1], 0.4),
+                                          "extra_seeds": STOCHASTIC_SEEDS}),
+    "checkered_sphere_dof_doughnut_100": ("scenes/checkered_sphere/checkered_sphere.yml",
+                                          {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
+                                           "aperture": (["DOUGHNUT_APERTURE", 1.0, 0.5], 0.4),
+                                           "extra_seeds": STOCHASTIC_SEEDS}),
+    "checkered_sphere_dof_square_100": ("scenes/checkered_sphere/checkered_sphere.yml",
+                                        {"size": (100, 100), "steps": (4, 4), "jitter": True, "threads": 1,
+                                         "aperture": (["SQUARE_APERTURE"], 0.4), "extra_seeds": STOCHASTIC_SEEDS}),
 }
+FIXTURE_YML = os.path.join(HERE, "yml")
 
 
 def find(items, pred):
@@ -126,6 +179,11 @@ def apply_overrides(tree, name, ov):
         if "aperture" in ov:  # (type list, size)
             ap = cam.setdefault("aperture", {})
             ap["type"], ap["size"] = ov["aperture"]
+    for cam in cams:
+        cam.update(ov.get("camera", {}))
+    for name_, fields in ov.get("define", {}).items():
+        for d in find(tree, lambda it: it.get("define") == name_):
+            d["value"].update(fields)
     if "cache" in ov:
         for light in find(tree, lambda it: it.get("add") == "light" and ("corner" in it or "radius" in it)):
             light["cache-size"] = ov["cache"]
@@ -176,8 +234,20 @@ def main(names):
 
     for name in names:
         yml_rel, ov = SCENES[name]
-        with open(os.path.join(REF_COPY, yml_rel)) as f:
+        yml_path = (os.path.join(FIXTURE_YML, yml_rel[4:]) if yml_rel.startswith("frt:")
+                    else os.path.join(REF_COPY, yml_rel))
+        with open(yml_path) as f:
             tree = yaml.safe_load(f)
+        for asset in ov.get("extra_assets", []):
+            # fixture data the scene loads at run time (our own files or the reference's scene data):
+            # into tests/golden/assets and the scratch reference copy the reference binary runs in
+            src = os.path.join(assets_dir, asset)
+            if not os.path.exists(src):
+                os.makedirs(os.path.dirname(src), exist_ok=True)
+                shutil.copyfile(os.path.join(REF_COPY, asset), src)
+            dst = os.path.join(REF_COPY, asset)
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            shutil.copyfile(src, dst)
         tree = apply_overrides(copy.deepcopy(tree), name, ov)
         yml_out = os.path.join(SCRATCH, name + ".yml")
         with open(yml_out, "w") as f:

@@ -41,7 +41,7 @@ main()
     /* config */
     struct global_config global_config;
     global_config.illumination.include_direct = True;
-    global_config.illumination.include_global = True;
+    global_config.illumination.include_global = False;
     global_config.illumination.debug_visualize_photon_map = False;
     global_config.illumination.debug_visualize_soft_indirect = False;
     global_config.illumination.di.include_ambient = False;
@@ -57,12 +57,12 @@ main()
     global_config.illumination.gi.irradiance_estimate_num = 200;
     global_config.illumination.gi.irradiance_estimate_radius = 0.1000000000;
     global_config.illumination.gi.irradiance_estimate_cone_filter_k = 1.0000000000;
-    global_config.illumination.gi.photon_count = 1000000;
+    global_config.illumination.gi.photon_count = 0;
     global_config.illumination.gi.path_length = 5;
 
     global_config.threading.num_threads = 8;
     global_config.scene.divide_threshold = 1;
-    global_config.output.file_path = "/tmp/frt_golden/out/cornell_gi_1920x1080_8x8";
+    global_config.output.file_path = "/tmp/frt_golden/out/cornell_direct_1920x1080_8x8";
     global_config.output.color_space = SRGB;
 
     void (*color_space_fn)(const Color, Color) = NULL;
@@ -115,7 +115,7 @@ main()
     Color area_light_0_intensity = color(1.0000000000, 1.0000000000, 1.0000000000);
     Vector area_light_0_uvec = vector_init(0.0000000000, 1.0000000000, 0.0000000000);
     Vector area_light_0_vvec = vector_init(0.0000000000, 0.0000000000, -1.0000000000);
-    area_light(area_light_0_corner, area_light_0_uvec, 10/*usteps*/, area_light_0_vvec, 10/*vsteps*/, true/*jitter*/, 65535/*cache_size*/, area_light_0_intensity, area_light_0);
+    area_light(area_light_0_corner, area_light_0_uvec, 10/*usteps*/, area_light_0_vvec, 10/*vsteps*/, true/*jitter*/, 1/*cache_size*/, area_light_0_intensity, area_light_0);
 
     /* end area light 0 */
 
