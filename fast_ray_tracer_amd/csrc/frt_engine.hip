@@ -1269,6 +1269,49 @@ static void build_walk_nodes(const frt_scene* sc, std::vector<frt::WalkNode>& wn
             }
             w.cN = std::nextafter((float)(n1 * (1.0 + 1e-9)), INFINITY);
             w.cT = std::nextafter((float)(tt * (1.0 + 1e-9)), INFINITY);
+            // axis-aligned frame (a signed permutation of the axes, up to entries below 2^-30 of a row's
+            // largest, such as the remnants of cos(pi/2) in a 90-degree rotation): world-space slab planes
+            // of cubes and finite composite boxes; local axis r tests world axis col[r]
+            const bool slab_node = nd.type == FRT_CUBE || nd.type == FRT_GROUP || nd.type == FRT_CSG;
+            bool aa = slab_node;
+            int col[3] = {0, 1, 2};
+            double small[3] = {0.0, 0.0, 0.0};
+            for (int r = 0; r < 3 && aa; ++r) {
+                int big = 0;
+                for (int q = 1; q < 3; ++q)
+                    if (std::fabs(c[4 * r + q]) > std::fabs(c[4 * r + big])) big = q;
+                const double cb = std::fabs(c[4 * r + big]);
+                if (!(cb > 0.0 && std::isfinite(cb))) aa = false;
+                for (int q = 0; q < 3; ++q)
+                    if (q != big) {
+                        if (!(std::fabs(c[4 * r + q]) <= 0x1p-30 * cb)) aa = false;
+                        small[r] += std::fabs(c[4 * r + q]);
+                    }
+                col[r] = big;
+            }
+            if (aa && (col[0] == col[1] || col[0] == col[2] || col[1] == col[2])) aa = false;
+            double bmax = 0.0, sig = 0.0;
+            for (int r = 0; r < 3 && aa; ++r) {
+                const int wa = col[r];
+                sig = std::max(sig, small[r] / std::fabs(c[4 * r + wa]));
+                const double crw = c[4 * r + wa], cr3 = c[4 * r + 3];
+                const double b0 = nd.type == FRT_CUBE ? -1.0 : nd.bbox[r], b1 = nd.type == FRT_CUBE ? 1.0 : nd.bbox[r + 3];
+                const double B0 = (b0 - cr3) / crw, B1 = (b1 - cr3) / crw;
+                if (!(std::isfinite(B0) && std::isfinite(B1) && std::isfinite(cr3))) {
+                    aa = false;
+                    break;
+                }
+                w.aab[wa] = (float)B0;
+                w.aab[wa + 3] = (float)B1;
+                if (!(std::isfinite(w.aab[wa]) && std::isfinite(w.aab[wa + 3]))) aa = false;
+                bmax = std::max({bmax, std::fabs((double)w.aab[wa]), std::fabs((double)w.aab[wa + 3])});
+                // |f32(d_w)| >= thr  =>  |local d_r| >= |c_rw d_w| - small_r >= EPSILON for the reference's
+                // direction (relative error of f32(d) <= 6.6u, of the composed map and the chain ~1e-15)
+                w.aathr[wa] = std::nextafter((float)((1e-5 + small[r]) / std::fabs(crw) * (1.0 + 1e-6)), INFINITY);
+            }
+            w.aa = aa ? 1 : 0;
+            w.aasig = aa && sig > 0.0 ? std::nextafter((float)(1.02 * sig), INFINITY) : 0.0f;
+            w.aabmax = aa ? std::nextafter((float)(bmax * (1.0 + 1e-7)), INFINITY) : 0.0f;
         }
         for (int r = 0; r < 3; ++r) {
             w.mrow_l1[r] = 0.f;
@@ -1676,28 +1719,39 @@ static void launch_shadow_redo_f(frt_scene_handle* h, const frt::Batch& B, const
 
 static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts) {
     if (h->jit_shadow) {
-        // scene-specialised kernel, then the generic walk over the lanes it handed back (usually none)
-        int64_t work = n * h->samples_per_node;
-        hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
-        void* args[] = {&h->S, (void*)&B, (void*)&rec, &n, &h->j_light, &h->j_point, &h->samples_per_node,
-                        &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
-        const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(work, frt::kTraceBlock), 1, 1,
-                                                    frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
-        if (le != hipSuccess) {
-            // the counts are still the zero memset: run the generic walk for this launch and the rest of
-            // the handle's life instead of rendering everything shadowed
-            std::fprintf(stderr, "frt: scene-specialised shadow kernel launch failed (%s); generic walk\n",
-                         hipGetErrorString(le));
-            (void)hipGetLastError();
-            h->jit_shadow = nullptr;
-            launch_shadow(h, B, rec, n, counts);
-            return;
-        }
-        switch (h->S.features & 3) {
-        case 0: launch_shadow_redo_f<0>(h, B, rec, n, counts); break;
-        case 1: launch_shadow_redo_f<1>(h, B, rec, n, counts); break;
-        case 2: launch_shadow_redo_f<2>(h, B, rec, n, counts); break;
-        default: launch_shadow_redo_f<3>(h, B, rec, n, counts); break;
+        // scene-specialised kernel (32-bit lane index: at most 2^31 lanes per launch), then the generic
+        // walk over the lanes it handed back (usually none)
+        const uint32_t spn = (uint32_t)h->samples_per_node;
+        uint32_t shift = 32;
+        while ((1u << (shift - 32)) < spn) ++shift;  // 32 + ceil(log2 spn)
+        const uint64_t magic = (uint64_t)((((unsigned __int128)1 << shift) + spn - 1) / spn);
+        const int64_t max_nodes = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / std::max<int64_t>(1, spn));
+        for (int64_t n0 = 0; n0 < n; n0 += max_nodes) {
+            const int64_t nc = std::min(max_nodes, n - n0);
+            const frt::ShadowHead* rc = rec + n0;
+            int32_t* cc = counts + n0 * h->S.num_lights;
+            uint32_t total = (uint32_t)(nc * spn);
+            hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
+            void* args[] = {&h->S, (void*)&B, (void*)&rc, &total, &h->j_light, &h->j_point, (void*)&spn, (void*)&magic,
+                            &shift, &cc, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
+            const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(total, frt::kTraceBlock),
+                                                        1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
+            if (le != hipSuccess) {
+                // the counts of this chunk are still the zero memset: run the generic walk for the rest of
+                // the launch and the rest of the handle's life instead of rendering everything shadowed
+                std::fprintf(stderr, "frt: scene-specialised shadow kernel launch failed (%s); generic walk\n",
+                             hipGetErrorString(le));
+                (void)hipGetLastError();
+                h->jit_shadow = nullptr;
+                launch_shadow(h, B, rc, n - n0, cc);
+                return;
+            }
+            switch (h->S.features & 3) {
+            case 0: launch_shadow_redo_f<0>(h, B, rc, nc, cc); break;
+            case 1: launch_shadow_redo_f<1>(h, B, rc, nc, cc); break;
+            case 2: launch_shadow_redo_f<2>(h, B, rc, nc, cc); break;
+            default: launch_shadow_redo_f<3>(h, B, rc, nc, cc); break;
+            }
         }
         return;
     }

@@ -100,21 +100,42 @@ __device__ __forceinline__ bool finite_ray(const Ray& r, double dist) {
 // undecidable comparison (or a direction component near the reference's
 // EPSILON slab branch) is marked `amb` and re-walked with the binary64 code.
 //
-// Error model (u = 2^-24, round to nearest; v_rcp_f32 within 1 ulp = 2u):
+// Error model (u = 2^-24, round to nearest; v_rcp_f32 / v_rsq_f32 within 1 ulp = 2u):
+//  * world ray (ray32): v = light point - over_point in binary64 (the reference's own subtraction),
+//    f32(v) (u), n2 = |f32(v)|^2 (<= 5u relative to |v|^2), rs = rsq(n2) (<= 2u + 2.5u),
+//    d~ = f32(v) rs: every component within 6.6u (relative) of the reference's v_a / |v|; the
+//    distance n2 rs within 5.6u of sqrt(v.v): DIST = dist~ (1 -+ 8u) (the product's rounding
+//    included); o~ = f32(over_point) (u).
 //  * frame: node k's ray = C_k (world ray), C_k = M_k ... M_1 composed in binary64 at upload,
 //    evaluated as a 3-term fma chain on binary32 operands. Against the reference's sequential
-//    binary64 transforms: |o - o_ref|_inf <= eo = 6u (cN |o_w|_inf + cT), |d - d_ref|_inf <= ed
-//    = 6u cN (|d_w|_inf <= 1, normalised) — 3u for the chain, u for each of the world-ray and
-//    matrix roundings, the reference's own rounding (~1e-16) and the bound's rounding in the rest.
+//    binary64 transforms: |o - o_ref|_inf <= eo = 6u (cN |o_w|_inf + cT) — 3u for the chain, u for
+//    each of the world-ray and matrix roundings, the reference's own rounding (~1e-16) and the
+//    bound's rounding in the rest; |d - d_ref|_inf <= ed = 12u cN (|d_w|_inf <= 1: the world
+//    direction's 6.6u in place of u).
 //  * slab value t = (b - o_a) / d_a: |t~ - t_ref| <= 4.2u |t~| + (eo + u |b|) / |d_ref| + |t~| ed / |d_ref|
 //    with 1 / |d_ref| <= 1 / (|d~_a| - ed); taken as 7u |t~| + ... and x1.01 on the
 //    rest, covering the roundings of the bound arithmetic and of the interval ends.
+//  * axis-aligned frame (C_k's 3x3 part diagonal, WalkNode::aa): the reference's local slab value
+//    (b - o'_a) / d'_a with o'_a = c_aa o_a + c_a3, d'_a = c_aa d_a equals t* = (B - o_a) / d_a,
+//    B = (b - c_a3) / c_aa, exactly in real arithmetic (its binary64 roundings are ~2^-50
+//    relative). On the world ray: r~ = rcp(d~) = (1 + eta) / d_a with |eta| <= 8.7u, o r~ rounded
+//    (u), B rounded to binary32 (u), t~ = fma(B~, r~, -o~ r~) rounded once (u):
+//    |t~ - t*| <= 1.01u |t~| + (9.7u |B| + 10.7u |o|) / |d_a|, |1 / d_a| <= |r~| (1 + 8.8u); taken
+//    as 2.5u |t~| + 12u (max|B| + max|o|) |r~|, the slack covering the roundings of the bound and
+//    of the interval ends and the reference's binary64 roundings. A signed permutation of the axes
+//    (90-degree rotations) is the same test on world axis col(a); its other entries (sigma <= 2^-29
+//    of the row's largest: remnants of cos(pi/2)) move t by <= 1.0001 sigma (|o| + |t|) |1 / d_a|:
+//    the |o| part lies inside K0's slack, the |t| part is added to K1 as aasig |r~|, and the
+//    EPSILON threshold includes them.
 //  * tmin = max of the axes' low values, tmax = min of the high ones: intervals of a max / min
 //    are the max / min of the intervals.
 constexpr float kU = 0x1p-24f;
 constexpr float kXfErr = 6.0f * kU;
+constexpr float kXfErrD = 12.0f * kU;
 constexpr float kSlabRel = 7.0f * kU;
 constexpr float kSlack = 1.01f;
+constexpr float kAaK1 = 2.5f * kU;
+constexpr float kAaK0 = 12.0f * kU;
 
 struct Iv {
     float lo, hi;
@@ -129,15 +150,119 @@ __device__ __forceinline__ Iv iv_of(double x) { return Iv{__double2float_rd(x), 
 
 struct World32 {
     float o[3], d[3], omax;
+    // shared by every axis-aligned slab test of the lane: rcp(d~), f32(o~ r~), 12u |r~|, 12u |r~| omax
+    float r[3], ro[3], P[3], Q[3];
 };
 
-__device__ __forceinline__ void world32(const Ray& r, World32& w) {
+__device__ __forceinline__ void world32_finish(World32& w) {
+    w.omax = fmaxf(fmaxf(fabsf(w.o[0]), fabsf(w.o[1])), fabsf(w.o[2]));
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        w.o[a] = (float)r.o[a];
-        w.d[a] = (float)r.d[a];
+        w.r[a] = __builtin_amdgcn_rcpf(w.d[a]);
+        w.ro[a] = w.o[a] * w.r[a];
+        w.P[a] = kAaK0 * fabsf(w.r[a]);
+        w.Q[a] = w.P[a] * w.omax;
     }
-    w.omax = fmaxf(fmaxf(fabsf(w.o[0]), fabsf(w.o[1])), fabsf(w.o[2]));
+}
+
+// ---- the shadow lane in 32-bit arithmetic ----
+// One lane per (path node, light sample j), as shadow_lane (frt_shadow.hpp): the host launches at
+// most 2^31 lanes per call, so the lane index is 32-bit and node = tid / spn is a multiply-shift
+// (magic = ceil(2^shift / spn), shift = 32 + ceil(log2 spn): exact for every 32-bit tid).
+struct Lane32 {
+    uint32_t node;
+    int light;
+    bool valid, live;
+    const double* lp;  // the light point (binary64)
+    const double* op;  // the path node's over_point
+};
+
+__device__ __forceinline__ void lane32(const DevScene& S, const Batch& B, const ShadowHead* __restrict__ shead,
+                                       uint32_t total, const int32_t* __restrict__ j_light,
+                                       const int32_t* __restrict__ j_point, uint32_t spn, uint64_t magic,
+                                       uint32_t shift, uint32_t tid, Lane32& L) {
+    L.valid = tid < total;
+    L.live = false;
+    L.node = 0;
+    L.light = 0;
+    L.lp = L.op = nullptr;
+    if (L.valid) {
+        L.node = (uint32_t)(((uint64_t)tid * magic) >> shift);
+        const uint32_t j = tid - L.node * spn;
+        L.light = j_light[j];
+        const int pt = j_point[j];
+        const ShadowHead* nr = shead + L.node;
+        if (nr->material >= 0) {
+            L.live = true;
+            const frt_light& lt = S.lights[L.light];
+            const int row = light_row(lt, B.seed, nr->key, L.light, 0);
+            L.lp = S.light_points + lt.points + 3 * ((int64_t)row * lt.num_samples + pt);
+            L.op = nr->over_point;
+        }
+    }
+}
+
+// is_shadowed's ray (renderer.c:74-93) in binary32 with the bounds of the error model above; false
+// when they cannot be given (non-finite or degenerate): the lane takes the binary64 walk
+__device__ __forceinline__ bool ray32(const Lane32& L, World32& w, Iv& dist) {
+    float vf[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        vf[a] = (float)(L.lp[a] - L.op[a]);
+        w.o[a] = (float)L.op[a];
+    }
+    const float n2 = vf[0] * vf[0] + vf[1] * vf[1] + vf[2] * vf[2];
+    const float rs = __builtin_amdgcn_rsqf(n2);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) w.d[a] = vf[a] * rs;
+    const float dl = n2 * rs;
+    dist = Iv{dl * (1.0f - 8.0f * kU), dl * (1.0f + 8.0f * kU)};
+    world32_finish(w);
+    return n2 >= 0x1p-60f && n2 <= 0x1p100f && w.omax <= 0x1p100f;  // (false for NaN)
+}
+
+// the reference's binary64 ray, exactly as shadow_lane computes it. Every lane of a wave runs the
+// blocks that call this (uniform branches), so lanes without a ray (padding, nodes without a hit)
+// get a placeholder instead of reading through their null light point.
+__device__ __forceinline__ void ray64(const Lane32& L, Ray& r, double& dist) {
+    if (!L.live) {
+        r = Ray{{0, 0, 0}, {0, 0, 1}};
+        dist = 0.0;
+        return;
+    }
+    double v[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        v[a] = L.lp[a] - L.op[a];
+        r.o[a] = L.op[a];
+    }
+    dist = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    normalize3(v, r.d);
+}
+
+// ray64 on a lane's first request (leaves the interval walk evaluates in binary64)
+__device__ __forceinline__ void ray64_once(const Lane32& L, bool& have, Ray& r, double& dist) {
+    if (!have) {
+        ray64(L, r, dist);
+        have = true;
+    }
+}
+
+// segmented wave reduction of the lit lanes (shadow_count with 32-bit keys)
+__device__ __forceinline__ void count32(const DevScene& S, const Lane32& L, bool lit, int32_t* counts) {
+    const int lane = threadIdx.x & 63;
+    const int key = L.valid ? (int)(L.node * (uint32_t)S.num_lights) + L.light : -1 - lane;
+    const int prev = __shfl_up(key, 1, 64);
+    const bool head = lane == 0 || prev != key;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long lits = __ballot(lit);
+    if (L.valid && head) {
+        const unsigned long long above = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
+        const int next = above ? __ffsll((long long)above) - 1 : 64;
+        const unsigned long long seg = (next >= 64 ? ~0ull : ((1ull << next) - 1)) & ~((1ull << lane) - 1);
+        const int c = __popcll(lits & seg);
+        if (c) atomicAdd(counts + key, c);
+    }
 }
 
 struct F32 {
@@ -152,7 +277,37 @@ __device__ __forceinline__ void frame32i(const WalkNode& nd, const World32& w, F
         f.d[r] = fmaf(c[0], w.d[0], fmaf(c[1], w.d[1], c[2] * w.d[2]));
     }
     f.eo = kXfErr * fmaf(nd.cN, w.omax, nd.cT);
-    f.ed = kXfErr * nd.cN;
+    f.ed = kXfErrD * nd.cN;
+}
+
+// the slab entries tmin / tmax of an axis-aligned node (WalkNode::aa) on the world ray; false when
+// |d_a| may be below the reference's EPSILON in the node's frame
+__device__ __forceinline__ bool aa_slab(const WalkNode& nd, const World32& w, Iv& tmin, Iv& tmax) {
+    bool ok = true;
+    float Ll = 0.0f, Lh = 0.0f, Hl = 0.0f, Hh = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        ok = ok && fabsf(w.d[a]) >= nd.aathr[a];
+        const float t0 = fmaf(nd.aab[a], w.r[a], -w.ro[a]);
+        const float t1 = fmaf(nd.aab[a + 3], w.r[a], -w.ro[a]);
+        const float e = fmaf(fmaxf(fabsf(t0), fabsf(t1)), fmaf(nd.aasig, fabsf(w.r[a]), kAaK1),
+                             fmaf(nd.aabmax, w.P[a], w.Q[a]));
+        const float mn = fminf(t0, t1), mx = fmaxf(t0, t1);
+        if (a == 0) {
+            Ll = mn - e;
+            Lh = mn + e;
+            Hl = mx - e;
+            Hh = mx + e;
+        } else {
+            Ll = fmaxf(Ll, mn - e);
+            Lh = fmaxf(Lh, mn + e);
+            Hl = fminf(Hl, mx - e);
+            Hh = fminf(Hh, mx + e);
+        }
+    }
+    tmin = Iv{Ll, Lh};
+    tmax = Iv{Hl, Hh};
+    return ok;
 }
 
 // the slab entries tmin / tmax as intervals; false when |d_a| may be below EPSILON
@@ -201,8 +356,24 @@ __device__ __forceinline__ int box_enter32(const WalkNode& nd, const F32& f, boo
     return 1;
 }
 
-// unit cube entries (cube.c:56-77): ex = 1 two entries, 0 none, -1 undecided
+// the same decision for an axis-aligned composite (WalkNode::aa), on the world ray
+__device__ __forceinline__ int box_enter_aa(const WalkNode& nd, const World32& w, bool skip_behind) {
+    Iv tmin, tmax;
+    if (!aa_slab(nd, w, tmin, tmax)) return -1;
+    const int hit = iv_le(tmin, tmax);
+    if (hit <= 0) return hit;
+    if (skip_behind && tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi))) return 0;
+    return 1;
+}
+
+// unit cube entries (cube.c:56-77): ex = 1 two entries, 0 none, -1 undecided; kAa: the cube's frame
+// is axis-aligned (world-space slab planes, no frame)
+template <bool kAa>
 __device__ __forceinline__ int cube_iv(const WalkNode& nd, const World32& w, Iv& t0, Iv& t1) {
+    if (kAa) {
+        if (!aa_slab(nd, w, t0, t1)) return -1;
+        return iv_le(t0, t1);
+    }
     F32 f;
     frame32i(nd, w, f);
     const float lo[3] = {-1.0f, -1.0f, -1.0f}, hi[3] = {1.0f, 1.0f, 1.0f};
@@ -211,10 +382,11 @@ __device__ __forceinline__ int cube_iv(const WalkNode& nd, const World32& w, Iv&
 }
 
 // a cube outside CSG units: leaf_top's decisions on intervals; undecided -> amb
+template <bool kAa>
 __device__ __forceinline__ void cube_top32(const WalkNode& nd, const World32& w, const Iv& dist, bool act, bool& alive,
                                            int& result, bool& any_entry, bool& amb) {
     Iv ta, tb;
-    const int ex = cube_iv(nd, w, ta, tb);
+    const int ex = cube_iv<kAa>(nd, w, ta, tb);
     if (!act) return;
     const int za = iv_le0(ta), zb = iv_le0(tb);
     const int la = iv_lt(ta, dist), lb = iv_lt(tb, dist);

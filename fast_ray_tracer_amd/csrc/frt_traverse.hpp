@@ -55,6 +55,17 @@ struct alignas(16) WalkNode {
     // |translation|, both rounded up
     float cm[12];
     float cN, cT;
+    // axis-aligned frames (the 3x3 part of the composed map a signed permutation up to entries below
+    // 2^-30 of their row's largest; written as if diagonal below, c_aa != 0): the node's slab
+    // planes in world coordinates, B = (b - c_a3) / c_aa for its two bounds b per axis (cube: -1 / +1,
+    // composite: its own-space box), rounded to binary32 — the slab test then runs on the world ray
+    // (frt_jit_rt.hpp aa_slab) without a frame or a reciprocal per node. aathr_a: |f32(d_a)| >= aathr_a
+    // proves the local |d_a| >= EPSILON (the reference's slab branch); aabmax >= every |B|; aasig >=
+    // 1.02 x (the other entries of a row / its largest), the relative error they add to t per |r_a|.
+    float aab[6];
+    float aathr[3];
+    float aabmax, aasig;
+    int32_t aa;
     int32_t pad2[2];
 };
 

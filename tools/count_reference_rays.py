@@ -16,6 +16,6 @@ for name in sys.argv[1:]:
     st["total"] = st["primary_rays"] + st["secondary_rays"] + st["shadow_rays"]
     st["oracle_seconds"] = round(time.time() - t, 2)
     idx = json.load(open(path))
-    idx[name]["reference_rays"] = st
+    idx.setdefault(name, {})["reference_rays"] = st
     json.dump(idx, open(path, "w"), indent=1, sort_keys=True)
     print(name, st, flush=True)
