@@ -154,6 +154,16 @@ struct World32 {
     float r[3], ro[3], P[3], Q[3];
 };
 
+// what the interval walk reads of a node, written into the generated kernel as a constexpr literal
+// per node (no loads; the fields are WalkNode's)
+struct Node32 {
+    float cm[12];
+    float cN, cT;
+    float bb32[6], bmag[3];
+    float aab[6], aathr[3], aabmax, aasig;
+    int casts;
+};
+
 __device__ __forceinline__ void world32_finish(World32& w) {
     w.omax = fmaxf(fmaxf(fabsf(w.o[0]), fabsf(w.o[1])), fabsf(w.o[2]));
 #pragma unroll
@@ -269,7 +279,7 @@ struct F32 {
     float o[3], d[3], eo, ed;
 };
 
-__device__ __forceinline__ void frame32i(const WalkNode& nd, const World32& w, F32& f) {
+__device__ __forceinline__ void frame32i(const Node32& nd, const World32& w, F32& f) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const float* c = nd.cm + 4 * r;
@@ -281,32 +291,32 @@ __device__ __forceinline__ void frame32i(const WalkNode& nd, const World32& w, F
 }
 
 // the slab entries tmin / tmax of an axis-aligned node (WalkNode::aa) on the world ray; false when
-// |d_a| may be below the reference's EPSILON in the node's frame
-__device__ __forceinline__ bool aa_slab(const WalkNode& nd, const World32& w, Iv& tmin, Iv& tmax) {
+// |d_a| may be below the reference's EPSILON in the node's frame. The two planes of an axis and the
+// two ends of the intervals travel as pairs (v_pk_fma_f32 / v_pk_add_f32).
+typedef float f2 __attribute__((ext_vector_type(2)));
+template <bool kSig>
+__device__ __forceinline__ bool aa_slab(const Node32& nd, const World32& w, Iv& tmin, Iv& tmax) {
     bool ok = true;
-    float Ll = 0.0f, Lh = 0.0f, Hl = 0.0f, Hh = 0.0f;
+    f2 lo = {0.0f, 0.0f}, hi = {0.0f, 0.0f};  // (tmin, tmax) lower ends, (tmin, tmax) upper ends
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         ok = ok && fabsf(w.d[a]) >= nd.aathr[a];
-        const float t0 = fmaf(nd.aab[a], w.r[a], -w.ro[a]);
-        const float t1 = fmaf(nd.aab[a + 3], w.r[a], -w.ro[a]);
-        const float e = fmaf(fmaxf(fabsf(t0), fabsf(t1)), fmaf(nd.aasig, fabsf(w.r[a]), kAaK1),
-                             fmaf(nd.aabmax, w.P[a], w.Q[a]));
-        const float mn = fminf(t0, t1), mx = fmaxf(t0, t1);
+        const f2 B = {nd.aab[a], nd.aab[a + 3]};
+        const f2 t = __builtin_elementwise_fma(B, f2{w.r[a], w.r[a]}, f2{-w.ro[a], -w.ro[a]});
+        const float k1 = kSig ? fmaf(nd.aasig, fabsf(w.r[a]), kAaK1) : kAaK1;
+        const float e = fmaf(fmaxf(fabsf(t.x), fabsf(t.y)), k1, fmaf(nd.aabmax, w.P[a], w.Q[a]));
+        const f2 m = {fminf(t.x, t.y), fmaxf(t.x, t.y)};
+        const f2 l = m - f2{e, e}, h = m + f2{e, e};
         if (a == 0) {
-            Ll = mn - e;
-            Lh = mn + e;
-            Hl = mx - e;
-            Hh = mx + e;
+            lo = l;
+            hi = h;
         } else {
-            Ll = fmaxf(Ll, mn - e);
-            Lh = fmaxf(Lh, mn + e);
-            Hl = fminf(Hl, mx - e);
-            Hh = fminf(Hh, mx + e);
+            lo = f2{fmaxf(lo.x, l.x), fminf(lo.y, l.y)};
+            hi = f2{fmaxf(hi.x, h.x), fminf(hi.y, h.y)};
         }
     }
-    tmin = Iv{Ll, Lh};
-    tmax = Iv{Hl, Hh};
+    tmin = Iv{lo.x, hi.x};
+    tmax = Iv{lo.y, hi.y};
     return ok;
 }
 
@@ -345,7 +355,7 @@ __device__ __forceinline__ bool slab_iv(const F32& f, const float* lo, const flo
 }
 
 // a composite's box (bounding_box.c:164-175) in its own frame: 1 enter, 0 skip, -1 undecided
-__device__ __forceinline__ int box_enter32(const WalkNode& nd, const F32& f, bool skip_behind) {
+__device__ __forceinline__ int box_enter32(const Node32& nd, const F32& f, bool skip_behind) {
     Iv tmin, tmax;
     const float bmax = fmaxf(fmaxf(nd.bmag[0], nd.bmag[1]), nd.bmag[2]);
     if (!slab_iv(f, nd.bb32, nd.bb32 + 3, bmax, tmin, tmax)) return -1;
@@ -356,50 +366,61 @@ __device__ __forceinline__ int box_enter32(const WalkNode& nd, const F32& f, boo
     return 1;
 }
 
-// the same decision for an axis-aligned composite (WalkNode::aa), on the world ray
-__device__ __forceinline__ int box_enter_aa(const WalkNode& nd, const World32& w, bool skip_behind) {
+// kAa (per node, fixed by the generator): 0 the node's own frame (frame32i + slab_iv), 1 an
+// axis-aligned frame (aa_slab on the world ray), 2 the same with the permutation's remnants (aasig)
+
+// the composite box decision (box_enter32) for an axis-aligned composite, on the world ray
+template <int kAa>
+__device__ __forceinline__ int box_enter_aa(const Node32& nd, const World32& w, bool skip_behind) {
     Iv tmin, tmax;
-    if (!aa_slab(nd, w, tmin, tmax)) return -1;
-    const int hit = iv_le(tmin, tmax);
-    if (hit <= 0) return hit;
+    if (!aa_slab<kAa == 2>(nd, w, tmin, tmax)) return -1;
+    if (tmin.lo > tmax.hi) return 0;
+    if (!(tmin.hi <= tmax.lo)) return -1;
     if (skip_behind && tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi))) return 0;
     return 1;
 }
 
-// unit cube entries (cube.c:56-77): ex = 1 two entries, 0 none, -1 undecided; kAa: the cube's frame
-// is axis-aligned (world-space slab planes, no frame)
-template <bool kAa>
-__device__ __forceinline__ int cube_iv(const WalkNode& nd, const World32& w, Iv& t0, Iv& t1) {
-    if (kAa) {
-        if (!aa_slab(nd, w, t0, t1)) return -1;
-        return iv_le(t0, t1);
-    }
+// unit cube slab intervals (cube.c:56-77); false: |d_a| may be below EPSILON
+template <int kAa>
+__device__ __forceinline__ bool cube_slab(const Node32& nd, const World32& w, Iv& t0, Iv& t1) {
+    if (kAa) return aa_slab<kAa == 2>(nd, w, t0, t1);
     F32 f;
     frame32i(nd, w, f);
     const float lo[3] = {-1.0f, -1.0f, -1.0f}, hi[3] = {1.0f, 1.0f, 1.0f};
-    if (!slab_iv(f, lo, hi, 1.0f, t0, t1)) return -1;
+    return slab_iv(f, lo, hi, 1.0f, t0, t1);
+}
+
+// unit cube entries: ex = 1 two entries, 0 none, -1 undecided
+template <int kAa>
+__device__ __forceinline__ int cube_iv(const Node32& nd, const World32& w, Iv& t0, Iv& t1) {
+    if (!cube_slab<kAa>(nd, w, t0, t1)) return -1;
     return iv_le(t0, t1);
 }
 
-// a cube outside CSG units: leaf_top's decisions on intervals; undecided -> amb
-template <bool kAa>
-__device__ __forceinline__ void cube_top32(const WalkNode& nd, const World32& w, const Iv& dist, bool act, bool& alive,
+// a cube outside CSG units: leaf_top's decisions on intervals, as lane masks; undecided -> amb.
+// With entries tmin <= tmax: the walk stops iff tmax > 0; the lane is blocked iff tmax < distance or
+// 0 < tmin < distance (an entry in (0, distance), intersection.c:42-55).
+template <int kAa>
+__device__ __forceinline__ void cube_top32(const Node32& nd, const World32& w, const Iv& dist, bool act, bool& alive,
                                            int& result, bool& any_entry, bool& amb) {
     Iv ta, tb;
-    const int ex = cube_iv<kAa>(nd, w, ta, tb);
+    const bool ok = cube_slab<kAa>(nd, w, ta, tb);
     if (!act) return;
-    const int za = iv_le0(ta), zb = iv_le0(tb);
-    const int la = iv_lt(ta, dist), lb = iv_lt(tb, dist);
-    if (ex < 0 || (ex > 0 && (za < 0 || zb < 0 || (za == 0 && la < 0) || (zb == 0 && lb < 0)))) {
+    const bool miss = ta.lo > tb.hi, hit = ta.hi <= tb.lo;
+    const bool stop = tb.lo > 0.0f, nostop = tb.hi <= 0.0f;
+    const bool max_in = tb.hi < dist.lo, max_out = tb.lo >= dist.hi;
+    const bool min_pos = ta.lo > 0.0f, min_nonpos = ta.hi <= 0.0f;
+    const bool min_in = ta.hi < dist.lo, min_out = ta.lo >= dist.hi;
+    const bool blk_known = max_in || (max_out && (min_nonpos || (min_pos && (min_in || min_out))));
+    if (!(ok && (miss || (hit && (nostop || (stop && blk_known)))))) {
         amb = true;
         alive = false;
         return;
     }
-    if (ex == 0) return;
+    if (miss) return;
     any_entry = true;
-    if (za == 0 || zb == 0) {  // an entry that is not <= 0 ends the walk
-        const bool blocked = (za == 0 && la == 1) || (zb == 0 && lb == 1);
-        result = blocked && nd.casts ? 1 : 0;
+    if (stop) {  // an entry that is not <= 0 ends the walk
+        result = (max_in || (min_pos && min_in)) && nd.casts ? 1 : 0;
         alive = false;
     }
 }
