@@ -1375,7 +1375,7 @@ int frt_jit_check(const frt_scene* sc, char* log, size_t log_cap, char* src, siz
     std::vector<frt::WalkNode> wn;
     build_walk_nodes(sc, wn);
     std::string why, clog;
-    const std::string code = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, why);
+    const std::string code = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, sc->lights, sc->num_lights, why);
     auto put = [](char* dst, size_t cap, const std::string& v) {
         if (dst && cap) {
             std::snprintf(dst, cap, "%s", v.c_str());
@@ -1435,7 +1435,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         const char* jit_env = std::getenv("FRT_JIT");
         if (rc == 0 && sc->config.include_direct && !(jit_env && std::strcmp(jit_env, "0") == 0)) {
             std::string why, log;
-            const std::string src = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, why);
+            const std::string src = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, sc->lights, sc->num_lights, why);
             if (!src.empty() && frt_jit_compile(src, h->device, &h->jit_shadow, log) != 0) {
                 why = "hiprtc: " + log.substr(0, 2000);
                 h->jit_shadow = nullptr;

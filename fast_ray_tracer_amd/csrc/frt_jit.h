@@ -8,11 +8,12 @@
 namespace frt {
 struct WalkNode;
 }
+struct frt_light;
 
-// HIP source of the shadow kernel for this tree ("" and `why` set when the scene
+// HIP source of the shadow kernel for this tree and these lights ("" and `why` set when the scene
 // is not eligible: too many nodes, or a CSG unit with a leaf whose list is unsorted)
 std::string frt_jit_shadow_source(const frt::WalkNode* wn, int num_nodes, const int32_t* roots, int num_roots,
-                                  std::string& why);
+                                  const frt_light* lights, int num_lights, std::string& why);
 
 // compile with hiprtc for `device` (cached per device and source); 0 on success, *fn = hipFunction_t
 int frt_jit_compile(const std::string& src, int device, void** fn, std::string& log);

@@ -214,12 +214,12 @@ __device__ __forceinline__ void lane32(const DevScene& S, const Batch& B, const 
 
 // is_shadowed's ray (renderer.c:74-93) in binary32 with the bounds of the error model above; false
 // when they cannot be given (non-finite or degenerate): the lane takes the binary64 walk
-__device__ __forceinline__ bool ray32(const Lane32& L, World32& w, Iv& dist) {
+__device__ __forceinline__ bool ray32v(const double* lp, const double* op, World32& w, Iv& dist) {
     float vf[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        vf[a] = (float)(L.lp[a] - L.op[a]);
-        w.o[a] = (float)L.op[a];
+        vf[a] = (float)(lp[a] - op[a]);
+        w.o[a] = (float)op[a];
     }
     const float n2 = vf[0] * vf[0] + vf[1] * vf[1] + vf[2] * vf[2];
     const float rs = __builtin_amdgcn_rsqf(n2);
@@ -230,6 +230,8 @@ __device__ __forceinline__ bool ray32(const Lane32& L, World32& w, Iv& dist) {
     world32_finish(w);
     return n2 >= 0x1p-60f && n2 <= 0x1p100f && w.omax <= 0x1p100f;  // (false for NaN)
 }
+
+__device__ __forceinline__ bool ray32(const Lane32& L, World32& w, Iv& dist) { return ray32v(L.lp, L.op, w, dist); }
 
 // the reference's binary64 ray, exactly as shadow_lane computes it. Every lane of a wave runs the
 // blocks that call this (uniform branches), so lanes without a ray (padding, nodes without a hit)

@@ -20,10 +20,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 // area-light cache row for (path node, light, draw): the reference draws
 // rand() % cache_len twice per (hit, light) (light.c:196, renderer.c:915);
 // with a single-row cache both are row 0, as in the reference
-__device__ __forceinline__ int light_row(const frt_light& L, uint64_t seed, uint64_t key, int light, int draw) {
-    if (L.rows <= 1) return 0;
+__device__ __forceinline__ int light_row_n(int rows, uint64_t seed, uint64_t key, int light, int draw) {
+    if (rows <= 1) return 0;
     uint64_t h = mix64(seed ^ mix64(key * 0x9e3779b97f4a7c15ULL + (uint64_t)(light * 2 + draw + 1)));
-    return (int)(h % (uint64_t)L.rows);
+    return (int)(h % (uint64_t)rows);
+}
+
+__device__ __forceinline__ int light_row(const frt_light& L, uint64_t seed, uint64_t key, int light, int draw) {
+    return light_row_n(L.rows, seed, key, light, draw);
 }
 
 // Ray queues of the levels are segmented: a block appends to segment
