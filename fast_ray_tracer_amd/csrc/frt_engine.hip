@@ -1072,6 +1072,8 @@ __global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, Cols<NodeRec> r
 // host side: scene upload, buffer management, frame driver, C ABI
 // ======================================================================
 
+constexpr size_t kJitStatWords = 64 * 32 + 4 * 512;
+
 struct frt_scene_handle {
     int device = 0;
     frt::DevScene S{};
@@ -1087,7 +1089,8 @@ struct frt_scene_handle {
     int64_t* redo = nullptr;           // lanes handed back to the generic walk
     unsigned* redo_count = nullptr;
     unsigned redo_cap = 0;
-    unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks
+    unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks;
+                                              // then {waves, lanes} per node (frt_jit_rt.hpp node_stat)
     // work buffers (grow on demand)
     struct Level {
         frt::Cols<frt::NodeRec> rec;
@@ -1310,6 +1313,35 @@ static void build_walk_nodes(const frt_scene* sc, std::vector<frt::WalkNode>& wn
                 w.aathr[wa] = std::nextafter((float)((1e-5 + small[r]) / std::fabs(crw) * (1.0 + 1e-6)), INFINITY);
             }
             w.aa = aa ? 1 : 0;
+            // a round sphere in the world: exact signed permutation (no remnants) with one |scale|
+            w.sph_ok = 0;
+            if (nd.type == FRT_SPHERE) {
+                bool ok = true;
+                int cl[3] = {-1, -1, -1};
+                for (int r = 0; r < 3 && ok; ++r) {
+                    int nz = 0;
+                    for (int q = 0; q < 3; ++q)
+                        if (c[4 * r + q] != 0.0) {
+                            ++nz;
+                            cl[r] = q;
+                        }
+                    ok = nz == 1 && std::isfinite(c[4 * r + cl[r]]) && std::isfinite(c[4 * r + 3]);
+                }
+                ok = ok && cl[0] != cl[1] && cl[0] != cl[2] && cl[1] != cl[2];
+                if (ok) {
+                    const double s0 = std::fabs(c[cl[0]]);
+                    ok = s0 > 0.0 && std::fabs(c[4 + cl[1]]) == s0 && std::fabs(c[8 + cl[2]]) == s0;
+                    for (int r = 0; r < 3 && ok; ++r) {
+                        const double cen = -c[4 * r + 3] / c[4 * r + cl[r]];
+                        w.sph[cl[r]] = (float)cen;
+                        ok = std::isfinite(w.sph[cl[r]]);
+                    }
+                    const double rad = 1.0 / s0;
+                    w.sph[3] = std::nextafter((float)(rad * (1.0 + 1e-6)), INFINITY);
+                    ok = ok && std::isfinite(w.sph[3]) && rad > 1e-30;
+                }
+                w.sph_ok = ok ? 1 : 0;
+            }
             w.aasig = aa && sig > 0.0 ? std::nextafter((float)(1.02 * sig), INFINITY) : 0.0f;
             w.aabmax = aa ? std::nextafter((float)(bmax * (1.0 + 1e-7)), INFINITY) : 0.0f;
         }
@@ -1451,12 +1483,12 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                 h->redo = (int64_t*)p;
                 h->redo_count = (unsigned*)(h->redo + h->redo_cap);
                 if (std::getenv("FRT_JIT_STATS")) {
-                    if (hipMalloc((void**)&h->jit_stats, 64 * 32 * sizeof(unsigned long long)) != hipSuccess) {
+                    if (hipMalloc((void**)&h->jit_stats, kJitStatWords * sizeof(unsigned long long)) != hipSuccess) {
                         frt_scene_release(h);
                         return fail("frt_scene_upload: jit stats allocation failed");
                     }
                     h->owned.push_back(h->jit_stats);
-                    hip_ignore(hipMemset(h->jit_stats, 0, 64 * 32 * sizeof(unsigned long long)));
+                    hip_ignore(hipMemset(h->jit_stats, 0, kJitStatWords * sizeof(unsigned long long)));
                 }
             } else if (std::getenv("FRT_JIT_VERBOSE")) {
                 std::fprintf(stderr, "frt: generic shadow walk (%s)\n", why.c_str());
@@ -1559,7 +1591,7 @@ void frt_scene_release(frt_scene_handle* h) {
     if (!h) return;
     hip_ignore(hipSetDevice(h->device));
     if (h->jit_stats) {
-        std::vector<unsigned long long> c(64 * 32);
+        std::vector<unsigned long long> c(kJitStatWords);
         if (hipMemcpy(c.data(), h->jit_stats, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
             unsigned long long live = 0, amb = 0;
             for (int j = 0; j < 64; ++j) {
@@ -1568,6 +1600,10 @@ void frt_scene_release(frt_scene_handle* h) {
             }
             std::fprintf(stderr, "frt jit stats: live shadow lanes %llu, re-walked in binary64 %llu (%.4f%%)\n", live, amb,
                          live ? 100.0 * (double)amb / (double)live : 0.0);
+            for (int k = 0; k < std::min(h->S.num_nodes, 512); ++k)
+                if (c[2048 + 2 * k])
+                    std::fprintf(stderr, "frt jit stats: node %d: %llu waves, %llu lanes tested; composites: %llu waves, %llu lanes entered\n",
+                                 k, c[2048 + 2 * k], c[2048 + 2 * k + 1], c[3072 + 2 * k], c[3072 + 2 * k + 1]);
         }
     }
     for (void* p : h->owned) hip_ignore(hipFree(p));

@@ -161,6 +161,7 @@ struct Node32 {
     float cN, cT;
     float bb32[6], bmag[3];
     float aab[6], aathr[3], aabmax, aasig;
+    float sph[4], sphc;  // round spheres: centre, radius (1 + 1e-6) rounded up, max |centre|
     int casts;
 };
 
@@ -257,6 +258,16 @@ __device__ __forceinline__ void ray64_once(const Lane32& L, bool& have, Ray& r, 
     if (!have) {
         ray64(L, r, dist);
         have = true;
+    }
+}
+
+// FRT_JIT_STATS diagnostics: per node, the waves and the lanes that take its test (after the 64 x 32
+// words of per-launch counters)
+__device__ __forceinline__ void node_stat(unsigned long long* js, int k, bool act) {
+    const unsigned long long m = __ballot(act);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(js + 2048 + 2 * k, 1ull);
+        atomicAdd(js + 2048 + 2 * k + 1, (unsigned long long)__popcll(m));
     }
 }
 
@@ -366,6 +377,27 @@ __device__ __forceinline__ int box_enter32(const Node32& nd, const F32& f, bool 
     // wholly behind the ray: an upper bound of tmax is behind (walk()'s behind(), in binary32)
     if (skip_behind && tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi))) return 0;
     return 1;
+}
+
+// A round sphere (WalkNode::sph_ok) that the lane's ray certainly misses: the reference's discriminant
+// (sphere.c:14-39) is then negative. With v = centre - o and |d| = 1, the line's distance from the
+// centre is |v x d|; in binary32, |v~ - v| <= u (|C| + |o|) + u |v~| and |d~ - d| <= 6.6u per
+// component, so each component of v~ x d~ (three roundings) is within ec = 2u (|C| + |o|) + 21u max|v~|
+// of v x d. |v~ x d~|^2 > (R' + 1.75 ec)^2 (1 + 16u) with R' >= R (1 + 1e-6) then proves a distance
+// above R (1 + 1e-6): the exact discriminant is below -8e-6 |d'|^2 while the reference's binary64
+// one errs by < 2^-47 |d'|^2 (|o'|^2 + 1), |o'| = |v| / R < 1e4 (and |o| / R < 1e8 for its transform).
+__device__ __forceinline__ bool sphere_miss32(const Node32& nd, const World32& w) {
+    float v[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = nd.sph[a] - w.o[a];
+    const float vmax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fabsf(v[2]));
+    const float cx = v[1] * w.d[2] - v[2] * w.d[1];
+    const float cy = v[2] * w.d[0] - v[0] * w.d[2];
+    const float cz = v[0] * w.d[1] - v[1] * w.d[0];
+    const float c2 = cx * cx + cy * cy + cz * cz;
+    const float ec = fmaf(21.0f * kU, vmax, 2.0f * kU * (nd.sphc + w.omax));
+    const float t = fmaf(1.75f, ec, nd.sph[3]);
+    return c2 > t * t * (1.0f + 16.0f * kU) && vmax < 1e4f * nd.sph[3] && w.omax < 1e8f * nd.sph[3];
 }
 
 // kAa (per node, fixed by the generator): 0 the node's own frame (frame32i + slab_iv), 1 an

@@ -66,7 +66,11 @@ struct alignas(16) WalkNode {
     float aathr[3];
     float aabmax, aasig;
     int32_t aa;
-    int32_t pad2[2];
+    // spheres whose frame is an exact signed permutation with one scale (a round sphere in the
+    // world): centre and radius x (1 + 1e-6) rounded up, for the interval walk's certain-miss test
+    // (frt_jit_rt.hpp sphere_miss32); sph_ok = 0 otherwise
+    int32_t sph_ok;
+    float sph[4];
 };
 
 // per-frame cache of the current ray: reciprocal direction (two Newton steps),
