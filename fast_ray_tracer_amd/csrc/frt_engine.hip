@@ -39,6 +39,7 @@
 #include "frt_jit.h"
 #include "frt_shade.hpp"
 #include "frt_shadow.hpp"
+#include "frt_jit_rt.hpp"
 #include "frt_cols.hpp"
 
 namespace frt {
@@ -1086,9 +1087,18 @@ struct frt_scene_handle {
     size_t lds_bytes = 0;  // dynamic LDS of the traversal kernels
     // scene-specialised shadow kernel (frt_jit.hip); nullptr: the generic k_shadow runs
     void* jit_shadow = nullptr;
+    void* jit_beam = nullptr;          // its pair kernel (frt_jit_beam)
+    bool jit_beam_on = true;           // FRT_JIT_BEAM=0: every pair is walked ray by ray (A/B)
+    const int32_t* light_psamp = nullptr;  // the parts' samples (frt_jit_light_parts), -1 padded
+    const float* light_aabb = nullptr; // per light, per cache row: the points' box (binary32, outward)
+    uint32_t* mixed = nullptr;         // mixed (node, light) pairs, kMixSegs segments
+    int64_t mixed_cap = 0;
+    unsigned* mcount = nullptr;        // the segments' counters (kMixSegs lines of kMixLine words)
+    std::vector<unsigned> host_mcount;
     int64_t* redo = nullptr;           // lanes handed back to the generic walk
     unsigned* redo_count = nullptr;
     unsigned redo_cap = 0;
+    unsigned long long uniform_stats[3] = {0, 0, 0};  // FRT_JIT_STATS: (node, light) pairs all lit / all shadowed / mixed
     unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks;
                                               // then {waves, lanes} per node (frt_jit_rt.hpp node_stat)
     // work buffers (grow on demand)
@@ -1468,9 +1478,10 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         if (rc == 0 && sc->config.include_direct && !(jit_env && std::strcmp(jit_env, "0") == 0)) {
             std::string why, log;
             const std::string src = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, sc->lights, sc->num_lights, why);
-            if (!src.empty() && frt_jit_compile(src, h->device, &h->jit_shadow, log) != 0) {
+            if (!src.empty() && frt_jit_compile(src, h->device, &h->jit_shadow, &h->jit_beam, log) != 0) {
                 why = "hiprtc: " + log.substr(0, 2000);
                 h->jit_shadow = nullptr;
+                h->jit_beam = nullptr;
             }
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
@@ -1482,6 +1493,51 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                 h->owned.push_back(p);
                 h->redo = (int64_t*)p;
                 h->redo_count = (unsigned*)(h->redo + h->redo_cap);
+                const char* beam_env = std::getenv("FRT_JIT_BEAM");
+                h->jit_beam_on = !(beam_env && std::strcmp(beam_env, "0") == 0);
+                // each light's parts (frt_jit_light_parts) and, per cache row, the box of each part's points,
+                // rounded outward to binary32
+                std::vector<float> box;
+                std::vector<int32_t> psamp;
+                const int PS = frt_jit_part_size();
+                for (int l = 0; l < sc->num_lights; ++l) {
+                    const frt_light& lt = sc->lights[l];
+                    std::vector<int32_t> order;
+                    const int np = frt_jit_light_parts(lt, sc->light_points, PS, order);
+                    psamp.insert(psamp.end(), order.begin(), order.end());
+                    for (int r = 0; r < std::max(1, lt.rows); ++r) {
+                        for (int p = 0; p < np; ++p) {
+                            double pl[3] = {INFINITY, INFINITY, INFINITY}, ph[3] = {-INFINITY, -INFINITY, -INFINITY};
+                            for (int k = 0; k < PS; ++k) {
+                                const int q = order[(size_t)p * PS + k];
+                                if (q < 0) continue;
+                                const double* pt = sc->light_points + lt.points + 3 * ((int64_t)r * lt.num_samples + q);
+                                for (int a = 0; a < 3; ++a) {
+                                    pl[a] = std::min(pl[a], pt[a]);
+                                    ph[a] = std::max(ph[a], pt[a]);
+                                }
+                            }
+                            for (int a = 0; a < 3; ++a) {
+                                float f = (float)pl[a];
+                                if ((double)f > pl[a]) f = std::nextafter(f, -INFINITY);
+                                box.push_back(f);
+                            }
+                            for (int a = 0; a < 3; ++a) {
+                                float f = (float)ph[a];
+                                if ((double)f < ph[a]) f = std::nextafter(f, INFINITY);
+                                box.push_back(f);
+                            }
+                        }
+                    }
+                }
+                h->light_psamp = upload(h, psamp.data(), psamp.size(), rc);
+                h->light_aabb = upload(h, box.data(), box.size(), rc);
+                if (rc || hipMalloc((void**)&h->mcount, frt::jit::kMixSegs * frt::jit::kMixLine * sizeof(unsigned)) != hipSuccess) {
+                    frt_scene_release(h);
+                    return fail("frt_scene_upload: light box / pair list allocation failed");
+                }
+                h->owned.push_back(h->mcount);
+                h->host_mcount.assign((size_t)frt::jit::kMixSegs * frt::jit::kMixLine, 0u);
                 if (std::getenv("FRT_JIT_STATS")) {
                     if (hipMalloc((void**)&h->jit_stats, kJitStatWords * sizeof(unsigned long long)) != hipSuccess) {
                         frt_scene_release(h);
@@ -1593,13 +1649,19 @@ void frt_scene_release(frt_scene_handle* h) {
     if (h->jit_stats) {
         std::vector<unsigned long long> c(kJitStatWords);
         if (hipMemcpy(c.data(), h->jit_stats, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
-            unsigned long long live = 0, amb = 0;
+            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0;
             for (int j = 0; j < 64; ++j) {
                 live += c[32 * j];
                 amb += c[32 * j + 1];
+                pairs += c[32 * j + 2];
+                mixed += c[32 * j + 3];
             }
+            std::fprintf(stderr, "frt jit stats: pair kernel: live pairs %llu, mixed %llu (%.2f%%)\n", pairs, mixed,
+                         pairs ? 100.0 * (double)mixed / (double)pairs : 0.0);
             std::fprintf(stderr, "frt jit stats: live shadow lanes %llu, re-walked in binary64 %llu (%.4f%%)\n", live, amb,
                          live ? 100.0 * (double)amb / (double)live : 0.0);
+            std::fprintf(stderr, "frt jit stats: (node, light) pairs: all lit %llu, all shadowed %llu, mixed %llu\n",
+                         h->uniform_stats[0], h->uniform_stats[1], h->uniform_stats[2]);
             for (int k = 0; k < std::min(h->S.num_nodes, 512); ++k)
                 if (c[2048 + 2 * k])
                     std::fprintf(stderr, "frt jit stats: node %d: %llu waves, %llu lanes tested; composites: %llu waves, %llu lanes entered\n",
@@ -1755,39 +1817,81 @@ static void launch_shadow_redo_f(frt_scene_handle* h, const frt::Batch& B, const
 
 static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts) {
     if (h->jit_shadow) {
-        // scene-specialised kernel (32-bit lane index: at most 2^31 lanes per launch), then the generic
-        // walk over the lanes it handed back (usually none)
-        const uint32_t spn = (uint32_t)h->samples_per_node;
+        // scene-specialised kernels: frt_jit_beam decides whole (node, light) pairs, frt_jit_shadow walks
+        // the rays of the mixed ones (32-bit lane index: at most 2^31 lanes per launch), then the
+        // generic walk takes the lanes handed back (non-finite rays, usually none)
+        using frt::jit::kMixLine;
+        using frt::jit::kMixSegs;
+        int64_t NP = 0;  // parts of frt_jit_part_size() samples per path node (frt_jit_beam)
+        for (const auto& L : h->host_lights) NP += std::max(1, (L.num_samples + frt_jit_part_size() - 1) / frt_jit_part_size());
+        const int64_t npairs = n * NP;
+        const int64_t nblocks = (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
+        uint32_t segcap = h->jit_beam_on ? (uint32_t)(((nblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock)
+                                         : (uint32_t)std::max<int64_t>(1, npairs);
+        if (grow(&h->mixed, h->mixed_cap, (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
+            (void)hipGetLastError();
+            h->jit_shadow = nullptr;
+            launch_shadow(h, B, rec, n, counts);
+            return;
+        }
+        uint64_t total_mixed = 0;
+        hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
+        if (h->jit_beam_on) {
+            uint32_t np = (uint32_t)npairs;
+            void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap,
+                             &h->err, &h->jit_stats};
+            const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1,
+                                                        1, frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
+            if (le != hipSuccess) {
+                std::fprintf(stderr, "frt: scene-specialised pair kernel launch failed (%s); every pair per ray\n",
+                             hipGetErrorString(le));
+                (void)hipGetLastError();
+                h->jit_beam_on = false;
+                launch_shadow(h, B, rec, n, counts);
+                return;
+            }
+            if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                               hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                hipStreamSynchronize(h->stream) != hipSuccess)
+                return;
+            for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
+        } else {
+            total_mixed = (uint64_t)npairs;  // every pair, in order (frt_jit_shadow's all_pairs)
+        }
+        uint32_t all_pairs = h->jit_beam_on ? 0u : 1u;
+        // lanes per pair (a part of frt_jit_part_size() samples); tid / lpp by multiply-shift
+        uint32_t lpp = (uint32_t)frt_jit_part_size();
         uint32_t shift = 32;
-        while ((1u << (shift - 32)) < spn) ++shift;  // 32 + ceil(log2 spn)
-        const uint64_t magic = (uint64_t)((((unsigned __int128)1 << shift) + spn - 1) / spn);
-        const int64_t max_nodes = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / std::max<int64_t>(1, spn));
-        for (int64_t n0 = 0; n0 < n; n0 += max_nodes) {
-            const int64_t nc = std::min(max_nodes, n - n0);
-            const frt::ShadowHead* rc = rec + n0;
-            int32_t* cc = counts + n0 * h->S.num_lights;
-            uint32_t total = (uint32_t)(nc * spn);
-            hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
-            void* args[] = {&h->S, (void*)&B, (void*)&rc, &total, &h->j_light, &h->j_point, (void*)&spn, (void*)&magic,
-                            &shift, &cc, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
+        while ((1u << (shift - 32)) < lpp) ++shift;  // 32 + ceil(log2 lpp)
+        const uint64_t magic = (uint64_t)((((unsigned __int128)1 << shift) + lpp - 1) / lpp);
+        uint32_t spn = (uint32_t)h->samples_per_node;
+        const uint64_t max_pairs = std::max<uint64_t>(1, ((1ull << 31) - 1) / lpp);
+        hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
+        for (uint64_t p0 = 0; p0 < total_mixed; p0 += max_pairs) {
+            const uint64_t pc = std::min<uint64_t>(max_pairs, total_mixed - p0);
+            uint32_t total = (uint32_t)(pc * lpp), m0 = (uint32_t)p0;
+            void* args[] = {&h->S, (void*)&B, (void*)&rec, &total, &m0, &h->mixed, &h->mcount, &segcap, &all_pairs,
+                            &h->light_psamp, &lpp, (void*)&magic,
+                            &shift, &spn, &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
             const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(total, frt::kTraceBlock),
                                                         1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
             if (le != hipSuccess) {
-                // the counts of this chunk are still the zero memset: run the generic walk for the rest of
-                // the launch and the rest of the handle's life instead of rendering everything shadowed
+                // the pair kernel may have written counts already: clear them and take the generic walk for
+                // this launch and the rest of the handle's life instead of rendering everything shadowed
                 std::fprintf(stderr, "frt: scene-specialised shadow kernel launch failed (%s); generic walk\n",
                              hipGetErrorString(le));
                 (void)hipGetLastError();
+                hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
                 h->jit_shadow = nullptr;
-                launch_shadow(h, B, rc, n - n0, cc);
+                launch_shadow(h, B, rec, n, counts);
                 return;
             }
-            switch (h->S.features & 3) {
-            case 0: launch_shadow_redo_f<0>(h, B, rc, nc, cc); break;
-            case 1: launch_shadow_redo_f<1>(h, B, rc, nc, cc); break;
-            case 2: launch_shadow_redo_f<2>(h, B, rc, nc, cc); break;
-            default: launch_shadow_redo_f<3>(h, B, rc, nc, cc); break;
-            }
+        }
+        switch (h->S.features & 3) {
+        case 0: launch_shadow_redo_f<0>(h, B, rec, n, counts); break;
+        case 1: launch_shadow_redo_f<1>(h, B, rec, n, counts); break;
+        case 2: launch_shadow_redo_f<2>(h, B, rec, n, counts); break;
+        default: launch_shadow_redo_f<3>(h, B, rec, n, counts); break;
         }
         return;
     }
@@ -2260,6 +2364,20 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 KTimer t(h, st, 1);
                 launch_shadow(h, B, L.head, n, L.counts);
                 FRT_HIP(hipGetLastError());
+            }
+            if (h->jit_stats && h->S.num_lights > 0) {  // FRT_JIT_STATS: (node, light) counts all-lit / all-shadowed / mixed
+                std::vector<int32_t> hc((size_t)n * h->S.num_lights);
+                std::vector<frt::ShadowHead> hh((size_t)n);
+                FRT_HIP(hipMemcpyAsync(hc.data(), L.counts, hc.size() * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+                FRT_HIP(hipMemcpyAsync(hh.data(), L.head, hh.size() * sizeof(frt::ShadowHead), hipMemcpyDeviceToHost, h->stream));
+                FRT_HIP(hipStreamSynchronize(h->stream));
+                for (int64_t i = 0; i < n; ++i) {
+                    if (hh[(size_t)i].material < 0) continue;
+                    for (int l = 0; l < h->S.num_lights; ++l) {
+                        const int32_t c = hc[(size_t)(i * h->S.num_lights + l)];
+                        h->uniform_stats[c == 0 ? 1 : (c == h->host_lights[(size_t)l].num_samples ? 0 : 2)]++;
+                    }
+                }
             }
             {
                 KTimer t(h, st, 2);

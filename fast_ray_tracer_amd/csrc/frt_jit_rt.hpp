@@ -261,6 +261,50 @@ __device__ __forceinline__ void ray64_once(const Lane32& L, bool& have, Ray& r, 
     }
 }
 
+// ---- the list of mixed (node, light) pairs ----
+// The beam kernel appends the pairs it cannot decide to kMixSegs segments (block b to segment
+// b % kMixSegs, one counter per 256-byte line: device-scope atomics on one address serialise); the
+// per-ray kernel finds its pair from the segment counts with a wave scan and a binary search.
+constexpr int kMixSegs = 64;
+constexpr int kMixLine = 64;  // 32-bit words per counter line
+
+__device__ __forceinline__ void mix_append(bool mix, uint32_t pair, uint32_t* __restrict__ mixed,
+                                           unsigned* __restrict__ mcount, uint32_t segcap, unsigned* __restrict__ err) {
+    const unsigned long long mm = __ballot(mix);
+    if (mm == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int seg = (int)(blockIdx.x % kMixSegs);
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(mcount + seg * kMixLine, (unsigned)__popcll(mm));
+    base = __shfl(base, 0, 64);
+    if (mix) {
+        const unsigned at = base + (unsigned)__popcll(mm & ((1ull << lane) - 1));
+        if (at < segcap) mixed[(size_t)seg * segcap + at] = pair;
+        else atomicOr(err, kErrQueueOverflow);
+    }
+}
+
+// (all lanes of the wave) mixed index m -> its slot in the segmented list
+__device__ __forceinline__ size_t mix_slot(uint32_t m, const unsigned* __restrict__ mcount, uint32_t segcap) {
+    const int lane = threadIdx.x & 63;
+    const unsigned c = min(mcount[lane * kMixLine], segcap);  // (an overflowed segment keeps its capacity)
+    unsigned incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const unsigned excl = incl - c;
+    int lo = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+        const int probe = lo + step;
+        const unsigned e = __shfl(excl, probe & 63, 64);
+        if (probe < 64 && e <= m) lo = probe;
+    }
+    return (size_t)lo * segcap + (m - __shfl(excl, lo, 64));
+}
+
 // FRT_JIT_STATS diagnostics: per node, the waves and the lanes that take its test (after the 64 x 32
 // words of per-launch counters)
 __device__ __forceinline__ void node_stat(unsigned long long* js, int k, bool act) {
@@ -331,6 +375,153 @@ __device__ __forceinline__ bool aa_slab(const Node32& nd, const World32& w, Iv& 
     tmin = Iv{lo.x, hi.x};
     tmax = Iv{lo.y, hi.y};
     return ok;
+}
+
+// ---- beams: every shadow ray of one (path node, light) at once ----
+// The rays of a (node, light) pair share the origin o and end at the light's points p_j (one cache
+// row). With D = p - o (unnormalised), the reference's t along the normalised direction is
+// t = |D| s with s = t* / |D| = (B - o_a) / D_a for a slab plane B; |D| > 0 is common to every value
+// of one ray, so the walk's decisions (t <= 0, t < distance = |D| (1 +- 2^-52), t_i <= t_j, tmin <=
+// tmax) are decisions on s, with DIST = 1 +- 1e-7. Over the pair, D_a lies in [Dlo_a, Dhi_a] (the
+// row's bounding box minus o, widened by the binary32 roundings); when that interval keeps one sign,
+// s = N / D_a (N = B - o_a) lies between N / Dlo_a and N / Dhi_a, so the interval walk's code, fed
+// with these intervals, takes a decision only when it holds for every ray of the pair. A decision it
+// cannot take for all of them marks the pair "mixed": its rays are walked one by one.
+//  * N~ = B~ - o~: |N~ - N| <= eN = 1.01u (max|B| + |o~_a|) + u |N~|; q = N~ rcp(D) within 4u |q|;
+//    s within 1.02 (4u |q| + eN max|1 / D_a|) (1 + 3u) of N / D_a, plus the permutation remnants'
+//    sigma (|o| + |s| |D|max) max|1 / D_a| (their |t| / |d_a| term in s units).
+//  * EPSILON: |d'_a| = |c D_a| / |D| >= EPSILON for every ray when min|D_a| >= aathr_a |D|max.
+struct Beam32 {
+    float o[3], omax;
+    float Dlo[3], Dhi[3];  // bounds of the rays' D_a, sign-definite when sgn[a]
+    float ilo[3], ihi[3];  // rcp(Dlo), rcp(Dhi)
+    float im[3];           // max |1 / D_a| (1 + 3u)
+    float Dmin[3];         // min |D_a| (0 unless sign-definite)
+    float M[3];            // max |D_a|
+    float Dn, Dnmin;       // |D| <= Dn, |D| >= Dnmin
+    bool sgn[3];
+};
+
+// the beam of origin op (binary64) and a light row's box [pl, ph] (binary32, rounded outward)
+__device__ __forceinline__ void beam32(const double* op, const float* pl, const float* ph, Beam32& w) {
+    float n2 = 0.0f, m2 = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w.o[a] = (float)op[a];
+        const float x0 = pl[a] - w.o[a], x1 = ph[a] - w.o[a];
+        const float eD = 2.0f * kU * (fabsf(w.o[a]) + fmaxf(fabsf(x0), fabsf(x1)));
+        w.Dlo[a] = x0 - eD;
+        w.Dhi[a] = x1 + eD;
+        w.sgn[a] = w.Dlo[a] > 0.0f || w.Dhi[a] < 0.0f;
+        w.ilo[a] = __builtin_amdgcn_rcpf(w.Dlo[a]);
+        w.ihi[a] = __builtin_amdgcn_rcpf(w.Dhi[a]);
+        w.im[a] = fmaxf(fabsf(w.ilo[a]), fabsf(w.ihi[a])) * (1.0f + 3.0f * kU);
+        const float M = fmaxf(fabsf(w.Dlo[a]), fabsf(w.Dhi[a]));
+        w.Dmin[a] = w.sgn[a] ? fminf(fabsf(w.Dlo[a]), fabsf(w.Dhi[a])) : 0.0f;
+        w.M[a] = M;
+        n2 = fmaf(M, M, n2);
+        m2 = fmaf(w.Dmin[a], w.Dmin[a], m2);
+    }
+    w.omax = fmaxf(fmaxf(fabsf(w.o[0]), fabsf(w.o[1])), fabsf(w.o[2]));
+    w.Dn = sqrtf(n2) * (1.0f + 8.0f * kU);
+    w.Dnmin = sqrtf(m2) * (1.0f - 8.0f * kU);
+}
+
+// the s intervals of a slab plane pair (B0, B1) on axis a: false when D_a may change sign or the
+// reference's EPSILON branch may apply to some ray
+// thr: the node's aathr_a (0: no EPSILON branch), bmax >= |B0|, |B1|, sig: the node's aasig
+//  * an origin strictly inside the slab (N0 < 0 < N1 with the error margin): every ray has mn <= 0 <= mx
+//    on this axis (for |d'_a| below EPSILON the reference's values are -inf / +inf), whatever the sign of
+//    D_a: used when D_a may change sign or come near EPSILON. Rays with D_a > 0 have mn = N0 / D_a <=
+//    N0 / M+ and mx = N1 / D_a >= N1 / M+ (M+ = max D_a), rays with D_a < 0 have mn <= -N1 / M- and
+//    mx >= -N0 / M- (M- = max -D_a). Remnants: numerators shrink by sigma |o|, denominators grow by
+//    sigma |D|.
+template <bool kSig>
+__device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, const Beam32& w, int a, float B0, float B1,
+                                          Iv& mn, Iv& mx) {
+    const bool ok = w.sgn[a] && w.Dmin[a] >= thr * w.Dn;
+    const float N0 = fminf(B0, B1) - w.o[a], N1 = fmaxf(B0, B1) - w.o[a];
+    const float eN = fmaf(1.01f * kU, bmax + fabsf(w.o[a]), kU * fmaxf(fabsf(N0), fabsf(N1)));
+    if (!ok) {
+        const float rs = eN + (kSig ? 1.01f * sig * w.omax : 0.0f);
+        const float r0 = -N0 - rs, r1 = N1 - rs;
+        const float ds = kSig ? 1.01f * sig * w.Dn : 0.0f;
+        const float Mp = fmaxf(w.Dhi[a], 0.0f) + ds, Mn = fmaxf(-w.Dlo[a], 0.0f) + ds;
+        const float f = 1.0f - 8.0f * kU;
+        // (x / 0 = +inf: no ray of that sign)
+        const float vmx = fminf(r1 / Mp, r0 / Mn) * f, vmn = fminf(r0 / Mp, r1 / Mn) * f;
+        mn = Iv{-__builtin_huge_valf(), -vmn};
+        mx = Iv{vmx, __builtin_huge_valf()};
+        return r0 > 0.0f && r1 > 0.0f && vmx > 0.0f && vmn > 0.0f;  // (false for NaN)
+    }
+    const float q00 = N0 * w.ilo[a], q01 = N0 * w.ihi[a], q10 = N1 * w.ilo[a], q11 = N1 * w.ihi[a];
+    const float qm = fmaxf(fmaxf(fabsf(q00), fabsf(q01)), fmaxf(fabsf(q10), fabsf(q11)));
+    float err = 1.02f * fmaf(4.0f * kU, qm, eN * w.im[a]);
+    if (kSig) err = fmaf(sig * w.im[a], fmaf(qm, w.Dn, w.omax) * 1.01f, err);
+    const float lo0 = fminf(q00, q01), hi0 = fmaxf(q00, q01), lo1 = fminf(q10, q11), hi1 = fmaxf(q10, q11);
+    mn = Iv{fminf(lo0, lo1) - err, fminf(hi0, hi1) + err};
+    mx = Iv{fmaxf(lo0, lo1) - err, fmaxf(hi0, hi1) + err};
+    return ok;
+}
+
+template <bool kSig>
+__device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& tmin, Iv& tmax) {
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        Iv mn, mx;
+        ok = beam_axis<kSig>(nd.aathr[a], nd.aabmax, nd.aasig, w, a, nd.aab[a], nd.aab[a + 3], mn, mx) && ok;
+        if (a == 0) {
+            tmin = mn;
+            tmax = mx;
+        } else {
+            tmin = Iv{fmaxf(tmin.lo, mn.lo), fmaxf(tmin.hi, mn.hi)};
+            tmax = Iv{fminf(tmax.lo, mx.lo), fminf(tmax.hi, mx.hi)};
+        }
+    }
+    return ok;
+}
+
+// frames that are not axis-aligned take no beam decision (their pairs are mixed)
+__device__ __forceinline__ void frame32i(const Node32&, const Beam32&, F32& f) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) f.o[a] = f.d[a] = 0.0f;
+    f.eo = 0.0f;
+    f.ed = __builtin_huge_valf();  // slab_iv: |d| - ed < EPSILON -> undecided
+}
+
+// "wholly behind": every ray's t = |D| s <= Dnmin s_hi < -1e-6 (1 + |t|) (walk()'s behind())
+__device__ __forceinline__ bool behind_all(const Iv& tmax, const World32&) {
+    return tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi));
+}
+__device__ __forceinline__ bool behind_all(const Iv& tmax, const Beam32& w) {
+    const float T = w.Dnmin * tmax.hi * (1.0f - 4.0f * kU);
+    return tmax.hi < 0.0f && T < -1.01e-6f * (1.0f + fabsf(T));
+}
+
+// a round sphere whose box every ray of the beam misses: the box, centre~ -+ (R' + 2u (|C~| + R') +
+// 1e-6 R') with R' = nd.sph[3] >= R (1 + 1e-6), holds the ball of radius R (1 + 1e-6) around the true
+// centre, so each line passes the centre at more than that (sphere_miss32's margin argument)
+__device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w) {
+    bool miss = false, ok = true;
+    Iv tmin{0.0f, 0.0f}, tmax{0.0f, 0.0f};
+    const float h = nd.sph[3] + fmaf(2.0f * kU, nd.sphc + nd.sph[3], 1e-6f * nd.sph[3]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        Iv mn, mx;
+        const float B0 = nd.sph[a] - h, B1 = nd.sph[a] + h;
+        ok = beam_axis<false>(0.0f, nd.sphc + h, 0.0f, w, a, B0, B1, mn, mx) && ok;
+        if (a == 0) {
+            tmin = mn;
+            tmax = mx;
+        } else {
+            tmin = Iv{fmaxf(tmin.lo, mn.lo), fmaxf(tmin.hi, mn.hi)};
+            tmax = Iv{fminf(tmax.lo, mx.lo), fminf(tmax.hi, mx.hi)};
+        }
+        ok = ok && fabsf(w.o[a] - nd.sph[a]) < 1e4f * nd.sph[3];
+    }
+    miss = tmin.lo > tmax.hi;
+    return ok && miss && w.omax < 1e8f * nd.sph[3];
 }
 
 // the slab entries tmin / tmax as intervals; false when |d_a| may be below EPSILON
@@ -404,19 +595,19 @@ __device__ __forceinline__ bool sphere_miss32(const Node32& nd, const World32& w
 // axis-aligned frame (aa_slab on the world ray), 2 the same with the permutation's remnants (aasig)
 
 // the composite box decision (box_enter32) for an axis-aligned composite, on the world ray
-template <int kAa>
-__device__ __forceinline__ int box_enter_aa(const Node32& nd, const World32& w, bool skip_behind) {
+template <int kAa, typename W>
+__device__ __forceinline__ int box_enter_aa(const Node32& nd, const W& w, bool skip_behind) {
     Iv tmin, tmax;
     if (!aa_slab<kAa == 2>(nd, w, tmin, tmax)) return -1;
     if (tmin.lo > tmax.hi) return 0;
     if (!(tmin.hi <= tmax.lo)) return -1;
-    if (skip_behind && tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi))) return 0;
+    if (skip_behind && behind_all(tmax, w)) return 0;
     return 1;
 }
 
 // unit cube slab intervals (cube.c:56-77); false: |d_a| may be below EPSILON
-template <int kAa>
-__device__ __forceinline__ bool cube_slab(const Node32& nd, const World32& w, Iv& t0, Iv& t1) {
+template <int kAa, typename W>
+__device__ __forceinline__ bool cube_slab(const Node32& nd, const W& w, Iv& t0, Iv& t1) {
     if (kAa) return aa_slab<kAa == 2>(nd, w, t0, t1);
     F32 f;
     frame32i(nd, w, f);
@@ -425,8 +616,8 @@ __device__ __forceinline__ bool cube_slab(const Node32& nd, const World32& w, Iv
 }
 
 // unit cube entries: ex = 1 two entries, 0 none, -1 undecided
-template <int kAa>
-__device__ __forceinline__ int cube_iv(const Node32& nd, const World32& w, Iv& t0, Iv& t1) {
+template <int kAa, typename W>
+__device__ __forceinline__ int cube_iv(const Node32& nd, const W& w, Iv& t0, Iv& t1) {
     if (!cube_slab<kAa>(nd, w, t0, t1)) return -1;
     return iv_le(t0, t1);
 }
@@ -434,8 +625,8 @@ __device__ __forceinline__ int cube_iv(const Node32& nd, const World32& w, Iv& t
 // a cube outside CSG units: leaf_top's decisions on intervals, as lane masks; undecided -> amb.
 // With entries tmin <= tmax: the walk stops iff tmax > 0; the lane is blocked iff tmax < distance or
 // 0 < tmin < distance (an entry in (0, distance), intersection.c:42-55).
-template <int kAa>
-__device__ __forceinline__ void cube_top32(const Node32& nd, const World32& w, const Iv& dist, bool act, bool& alive,
+template <int kAa, typename W>
+__device__ __forceinline__ void cube_top32(const Node32& nd, const W& w, const Iv& dist, bool act, bool& alive,
                                            int& result, bool& any_entry, bool& amb) {
     Iv ta, tb;
     const bool ok = cube_slab<kAa>(nd, w, ta, tb);

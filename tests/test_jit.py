@@ -30,17 +30,21 @@ def test_jit_source_compiles(built, name):
         assert rc in (0, 1)
 
 
-def _render(name, jit, **kw):
+def _render(name, jit, beam=True, **kw):
+    """Render with the specialised kernels (jit; beam: with the (node, light) pair kernel) or the
+    generic walk; the switches are read at upload."""
     from fast_ray_tracer_amd.runtime import GpuRenderer
-    old = os.environ.get("FRT_JIT")
-    os.environ["FRT_JIT"] = "1" if jit else "0"
+    env = {"FRT_JIT": "1" if jit else "0", "FRT_JIT_BEAM": "1" if beam else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         r = GpuRenderer(load_scene(name))
     finally:
-        if old is None:
-            del os.environ["FRT_JIT"]
-        else:
-            os.environ["FRT_JIT"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     try:
         return r.render(stats=True, **kw)
     finally:
@@ -66,3 +70,26 @@ def test_jit_equals_generic_walk_on_benchmark_rows(built):
     img_g, _ = _render("cornell_direct_800_4x4", False, row_begin=300, row_end=340)
     assert st_j.shadow_jit == 1
     assert np.array_equal(img_j, img_g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "cornell_shipped_48_4x4", "reflect_refract_test_150",
+                                  "test_scene_120", "checkered_sphere_200"])
+def test_pair_kernel_equals_per_ray_walk(built, name):
+    """frt_jit_beam decides whole (node, light) pairs; the counts it writes must equal what the per-ray
+    walk gives for every ray of the pair: the canvas with and without it, bit for bit."""
+    img_b, st_b = _render(name, True, beam=True)
+    img_r, st_r = _render(name, True, beam=False)
+    assert np.array_equal(img_b, img_r)
+
+
+@pytest.mark.gpu
+def test_pair_kernel_on_headline_rows(built):
+    """The headline workload (cornell 1920x1080, 8x8 CMJ): row bands through the pair kernel, the
+    per-ray kernel alone and the generic walk, bit for bit."""
+    for rows in ((200, 208), (640, 648)):
+        img_b, st_b = _render("cornell_direct_1920x1080_8x8", True, beam=True, row_begin=rows[0], row_end=rows[1])
+        img_r, _ = _render("cornell_direct_1920x1080_8x8", True, beam=False, row_begin=rows[0], row_end=rows[1])
+        img_g, _ = _render("cornell_direct_1920x1080_8x8", False, row_begin=rows[0], row_end=rows[1])
+        assert st_b.shadow_jit == 1
+        assert np.array_equal(img_b, img_r) and np.array_equal(img_b, img_g)
