@@ -1098,6 +1098,9 @@ struct frt_scene_handle {
     int64_t* redo = nullptr;           // lanes handed back to the generic walk
     unsigned* redo_count = nullptr;
     unsigned redo_cap = 0;
+    frt_frame_stats* cur_st = nullptr;  // the instrumented frame's stats (sub-kernel timers), else null
+    uint64_t rays_walked = 0;           // shadow rays walked one by one in this frame
+    uint64_t pairs_walked = 0;          // (node, light part) pairs they belong to
     unsigned long long uniform_stats[3] = {0, 0, 0};  // FRT_JIT_STATS: (node, light) pairs all lit / all shadowed / mixed
     unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks;
                                               // then {waves, lanes} per node (frt_jit_rt.hpp node_stat)
@@ -1772,8 +1775,13 @@ static void collect_timings(frt_scene_handle* h, frt_frame_stats* st) {
     for (const auto& m : h->ev_marks) {
         float ms = 0.f;
         hip_ignore(hipEventElapsedTime(&ms, h->ev_pool[m.a], h->ev_pool[m.b]));
-        st->kernel_ms[m.slot] += ms;
-        st->kernel_launches[m.slot] += 1;
+        if (m.slot < 8) {
+            st->kernel_ms[m.slot] += ms;
+            st->kernel_launches[m.slot] += 1;
+        } else {
+            st->sub_ms[m.slot - 8] += ms;
+            st->sub_launches[m.slot - 8] += 1;
+        }
     }
     h->ev_marks.clear();
     h->ev_used = 0;
@@ -1840,8 +1848,12 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
             uint32_t np = (uint32_t)npairs;
             void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap,
                              &h->err, &h->jit_stats};
-            const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1,
-                                                        1, frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
+            hipError_t le;
+            {
+                KTimer tb(h, h->cur_st, 8);
+                le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1, 1,
+                                           frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
+            }
             if (le != hipSuccess) {
                 std::fprintf(stderr, "frt: scene-specialised pair kernel launch failed (%s); every pair per ray\n",
                              hipGetErrorString(le));
@@ -1867,6 +1879,9 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         uint32_t spn = (uint32_t)h->samples_per_node;
         const uint64_t max_pairs = std::max<uint64_t>(1, ((1ull << 31) - 1) / lpp);
         hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
+        h->rays_walked += total_mixed * lpp;  // (parts of fewer samples count their padding lanes too)
+        h->pairs_walked += total_mixed;
+        KTimer tr(h, h->cur_st, 9);
         for (uint64_t p0 = 0; p0 < total_mixed; p0 += max_pairs) {
             const uint64_t pc = std::min<uint64_t>(max_pairs, total_mixed - p0);
             uint32_t total = (uint32_t)(pc * lpp), m0 = (uint32_t)p0;
@@ -2200,10 +2215,16 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
             frt::Batch Bg = B;  // the gather rays form one contiguous queue
             Bg.qprefix = nullptr;
             launch_trace(h, Bg, G.gq, rays, G.ghits, 0);
-            hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_gather_hit<true> : k_gather_hit<false>, dim3(grid_for(rays)),
-                               dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq, G.ghits, rays, G.greq);
-            hipLaunchKernelGGL(k_gather_est, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, G.greq, rays,
-                               G.gcol);
+            {
+                KTimer th(h, st, 11);
+                hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_gather_hit<true> : k_gather_hit<false>, dim3(grid_for(rays)),
+                                   dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq, G.ghits, rays, G.greq);
+            }
+            {
+                KTimer te(h, st, 10);
+                hipLaunchKernelGGL(k_gather_est, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, G.greq, rays,
+                                   G.gcol);
+            }
             hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
                                G.fgather);
             FRT_HIP(hipGetLastError());
@@ -2256,6 +2277,9 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
 // a failed frame leaves no half-built state behind: photon maps traced by it (maybe truncated by a
 // store overflow) are not reused by the next frame with the same seed
 static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* dev_out, frt_frame_stats* st) {
+    h->cur_st = st;
+    h->rays_walked = 0;
+    h->pairs_walked = 0;
     const int rc = render_frame(h, P, dev_out, st);
     if (rc) h->gi.built = false;
     return rc;
@@ -2453,11 +2477,15 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->pruned_secondary = pruned;
         st->hits = hits;
         st->shadow_rays = h->S.cfg.include_direct ? hits * (uint64_t)h->samples_per_node : 0;
-        // DESIGN.md byte model: per shaded node its 64-byte ShadowHead read + one 4-byte count per light written
-        st->shadow_kernel_bytes =
-            h->S.cfg.include_direct && h->samples_per_node > 0 ? (double)hits * (64.0 + 4.0 * h->S.num_lights) : 0.0;
+        // DESIGN.md byte model of the per-ray shadow kernel: per walked (node, light part) pair its 4-byte list
+        // entry and the node's 64-byte ShadowHead read, one 4-byte count written; the generic walk: per shaded
+        // node the ShadowHead + one 4-byte count per light
+        st->shadow_kernel_bytes = !(h->S.cfg.include_direct && h->samples_per_node > 0) ? 0.0
+                                  : h->jit_shadow != nullptr ? (double)h->pairs_walked * (4.0 + 64.0 + 4.0)
+                                                             : (double)hits * (64.0 + 4.0 * h->S.num_lights);
         st->errors = err;
         st->shadow_jit = h->jit_shadow != nullptr ? 1 : 0;
+        st->shadow_rays_walked = h->jit_shadow != nullptr ? h->rays_walked : st->shadow_rays;
         collect_timings(h, st);
     }
 #if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)

@@ -35,10 +35,13 @@ class FrameStats(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_uint64 * 8),
                 ("shadow_kernel_bytes", ctypes.c_double), ("gather_rays", ctypes.c_uint64),
                 ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double),
-                ("shadow_jit", ctypes.c_int32), ("photon_pass", ctypes.c_int32)]
+                ("shadow_jit", ctypes.c_int32), ("photon_pass", ctypes.c_int32),
+                ("sub_ms", ctypes.c_double * 8), ("sub_launches", ctypes.c_uint64 * 8),
+                ("shadow_rays_walked", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
+        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
@@ -49,6 +52,9 @@ class FrameStats(ctypes.Structure):
             "photon_pass": int(self.photon_pass),
             "kernel_ms": {names[i]: float(self.kernel_ms[i]) for i in range(8) if self.kernel_launches[i]},
             "kernel_launches": {names[i]: int(self.kernel_launches[i]) for i in range(8) if self.kernel_launches[i]},
+            "sub_ms": {subs[i]: float(self.sub_ms[i]) for i in range(len(subs)) if self.sub_launches[i]},
+            "sub_launches": {subs[i]: int(self.sub_launches[i]) for i in range(len(subs)) if self.sub_launches[i]},
+            "shadow_rays_walked": int(self.shadow_rays_walked),
         }
 
 

@@ -216,6 +216,12 @@ typedef struct frt_frame_stats {
     double photon_ms;             /* photon tracing + map build of this frame (0 when the maps were reused) */
     int32_t shadow_jit;           /* 1: the scene-specialised shadow kernel ran (frt_jit.hip), 0: the generic walk */
     int32_t photon_pass;          /* 1: this frame traced its photon maps (a new seed), 0: maps reused / no GI */
+    /* kernels inside the slots above (HIP events around each launch on the engine stream):
+       0 frt_jit_beam (pair kernel), 1 frt_jit_shadow (per-ray kernel), 2 k_gather_est, 3 k_gather_hit */
+    double sub_ms[8];
+    uint64_t sub_launches[8];
+    uint64_t shadow_rays_walked;  /* shadow rays walked one by one; the rest of shadow_rays were resolved
+                                     (exactly, for every ray) per (node, light part) by frt_jit_beam */
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */
