@@ -175,7 +175,10 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
     found = latest_pmc(kname, workload)
     if found:
         path, t = found
-        roof["traffic"] = round(t["traffic_bytes_per_launch"])
+        if "traffic_bytes_per_launch" in t:
+            roof["traffic"] = round(t["traffic_bytes_per_launch"])
+        else:  # FETCH_SIZE + WRITE_SIZE (tools/pmc_summary.py, KiB units already converted)
+            roof["traffic"] = round(t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0))
         roof["traffic_source"] = os.path.relpath(path, ROOT)
         if "rocprof_avg_ms" in t:
             roof["rocprof_avg_launch_ms"] = round(t["rocprof_avg_ms"], 4)

@@ -1026,6 +1026,26 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 
         for (int k = 0; k < 3; ++k) gather_col[3 * t + k] = mine[k];
 }
 
+// frt_pm_estimate's kernel: one wave per query (pos[3], normal[3]), the estimate as lighting_gi
+// calls it before its scaling
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) k_pm_estimate(
+    PhotonMapDev M, const double* __restrict__ q, int64_t nq, double radius, int k, double cone_k,
+    double* __restrict__ irrad, int64_t* __restrict__ found) {
+    FRT_EST_LDS(lds, kGatherEstCap);
+    const int64_t w = ((int64_t)blockIdx.x * blockDim.x) / 64 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (w >= nq) return;  // (whole waves)
+    double x[3], nrm[3], e[3];
+    for (int j = 0; j < 3; ++j) {
+        x[j] = q[6 * w + j];
+        nrm[j] = q[6 * w + 3 + j];
+    }
+    const int64_t used = wave_irradiance_estimate(M, x, nrm, radius, k, cone_k, e, lds);
+    if (est_lane() == 0) {
+        for (int j = 0; j < 3; ++j) irrad[3 * w + j] = e[j];
+        found[w] = used;
+    }
+}
+
 // final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd
 __global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, Cols<NodeRec> rec, int64_t node0,
                                                           int64_t nodes, const double* __restrict__ gather_col,
@@ -2066,31 +2086,143 @@ static void quantized_dir(const double* d, double* out) {
     out[2] = T.ct[theta];
 }
 
+// ---- the reference's kd-tree (pm_balance, pm.c:329-494), restated ----
+// The estimate's exact selection (frt_gi.hpp) needs each photon's place in Jensen's balanced heap:
+// the photons the reference's search never reaches (pm.c:172 with half_stored_photons = n/2 - 1,
+// pm.c:372) and, for the first heap overflow of pm_locate_photons, the near-first traversal order
+// (split planes and positions of the internal nodes). Same median split (Sedgewick's partition),
+// same median choice and split axis from the shrinking bounding box; the two halves of a segment are
+// independent, so the first levels run on host threads. Checked against the reference's own
+// balanced maps (tests/test_photon_map.py, fixture tests/golden/pm_cornell_10k.npz).
+struct PmBalance {
+    const double* pos;  // 3 per stored photon, stored index 1..n at pos + 3 * (i - 1)
+    std::vector<int32_t> porg, pbal;
+    std::vector<int8_t> plane;
+    double at(int32_t i, int a) const { return pos[3 * (size_t)(i - 1) + a]; }
+    void median_split(int start, int end, int median, int axis) {
+        int left = start, right = end;
+        while (right > left) {
+            const double v = at(porg[(size_t)right], axis);
+            int i = left - 1, j = right;
+            for (;;) {
+                while (at(porg[(size_t)++i], axis) < v) {
+                }
+                while (at(porg[(size_t)--j], axis) > v && j > left) {
+                }
+                if (i >= j) break;
+                std::swap(porg[(size_t)i], porg[(size_t)j]);
+            }
+            std::swap(porg[(size_t)i], porg[(size_t)right]);
+            if (i >= median) right = i - 1;
+            if (i <= median) left = i + 1;
+        }
+    }
+    void segment(int64_t index, int start, int end, std::array<double, 3> bmin, std::array<double, 3> bmax, int spawn) {
+        int median = 1;
+        while (4 * median <= end - start + 1) median += median;
+        if (3 * median <= end - start + 1) {
+            median += median;
+            median += start - 1;
+        } else {
+            median = end - median + 1;
+        }
+        int axis = 2;
+        if (bmax[0] - bmin[0] > bmax[1] - bmin[1] && bmax[0] - bmin[0] > bmax[2] - bmin[2]) axis = 0;
+        else if (bmax[1] - bmin[1] > bmax[2] - bmin[2]) axis = 1;
+        median_split(start, end, median, axis);
+        pbal[(size_t)index] = porg[(size_t)median];
+        plane[(size_t)index] = (int8_t)axis;
+        const double split = at(porg[(size_t)median], axis);
+        std::thread left_thread;
+        if (median > start) {
+            if (start < median - 1) {
+                auto bmax2 = bmax;
+                bmax2[axis] = split;
+                if (spawn > 0)
+                    left_thread = std::thread([=]() { segment(2 * index, start, median - 1, bmin, bmax2, spawn - 1); });
+                else
+                    segment(2 * index, start, median - 1, bmin, bmax2, 0);
+            } else {
+                pbal[(size_t)(2 * index)] = porg[(size_t)start];
+            }
+        }
+        if (median < end) {
+            if (median + 1 < end) {
+                auto bmin2 = bmin;
+                bmin2[axis] = split;
+                segment(2 * index + 1, median + 1, end, bmin2, bmax, spawn > 0 ? spawn - 1 : 0);
+            } else {
+                pbal[(size_t)(2 * index + 1)] = porg[(size_t)end];
+            }
+        }
+        if (left_thread.joinable()) left_thread.join();
+    }
+};
+
+// heap_of[i] = heap index (1..n) of stored photon i (0-based), plane[h] = split axis of heap node h
+static void pm_balance_heap(const double* pos, int64_t n, std::vector<int32_t>& heap_of, std::vector<int8_t>& plane) {
+    heap_of.assign((size_t)n, 1);
+    plane.assign((size_t)n + 1, 0);
+    if (n <= 1) return;
+    PmBalance B;
+    B.pos = pos;
+    B.porg.resize((size_t)n + 1);
+    B.pbal.assign((size_t)n + 1, 0);
+    B.plane.assign((size_t)n + 1, 0);
+    for (int64_t i = 0; i <= n; ++i) B.porg[(size_t)i] = (int32_t)i;
+    std::array<double, 3> bmin{INFINITY, INFINITY, INFINITY}, bmax{-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a) {  // pm_store's bounding box (pm.c:277-284)
+            bmin[(size_t)a] = std::min(bmin[(size_t)a], pos[3 * i + a]);
+            bmax[(size_t)a] = std::max(bmax[(size_t)a], pos[3 * i + a]);
+        }
+    const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    int spawn = 0;
+    while ((1 << spawn) < threads && n > 65536) ++spawn;
+    B.segment(1, 1, (int)n, bmin, bmax, spawn);
+    for (int64_t h = 1; h <= n; ++h) heap_of[(size_t)(B.pbal[(size_t)h] - 1)] = (int32_t)h;
+    plane.swap(B.plane);
+}
+
 // dense uniform grid over the photons (frt_gi.hpp wave_scan_cells): cell edge
 // radius / 3, doubled while the grid would exceed kMaxGridCells; photons sorted
 // by cell, x fastest (a row of cells is one contiguous range); one allocation
 // per map: binary32 positions | power + direction records | cell starts
 constexpr double kMaxGridCells = (double)(1 << 24);
 
-static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::StoredPhoton>& ph, double scale) {
-    auto& G = h->gi;
-    hip_ignore(hipFree(G.map_mem[m]));
-    G.map_mem[m] = nullptr;
-    frt::PhotonMapDev M{};
-    const int64_t n = (int64_t)ph.size();
+// One photon map on the device from photons in the reference's storage order (positions, scaled powers,
+// pm_photon_dir directions): balanced as pm_balance would (heap index per photon, split planes), the
+// photons the reference's search reaches binned into the dense grid (frt_gi.hpp wave_scan_cells; cell
+// edge radius / 3, doubled while the grid would exceed kMaxGridCells; sorted by cell, x fastest, so a
+// row of cells is one contiguous range). One allocation per map: binary32 positions with the heap
+// index in .w | power + direction records | cell starts | the kd-tree (binary64 position and split
+// plane per heap index: the exact distances and the traversal order of the estimate).
+static int make_photon_map(int64_t n, const double* pos, const double* power, const double* dir,
+                           double irradiance_radius, void** out_mem, frt::PhotonMapDev& M) {
+    *out_mem = nullptr;
+    M = frt::PhotonMapDev{};
     if (n > ((int64_t)1 << 30)) return fail("photon map too large");
-    M.count = n;
+    std::vector<int32_t> heap_of;
+    std::vector<int8_t> plane;
+    pm_balance_heap(pos, n, heap_of, plane);
+    const int64_t half = n / 2 - 1;  // pm_balance's half_stored_photons (pm.c:372)
+    auto reachable = [&](int64_t hx) { return hx == 1 || (hx >> 1) < half; };
     double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};
     bool first = true;
-    for (const auto& p : ph) {
-        if (!(std::isfinite(p.pos[0]) && std::isfinite(p.pos[1]) && std::isfinite(p.pos[2]))) continue;
+    int64_t nr = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!reachable(heap_of[(size_t)i])) continue;
+        ++nr;
+        const double* p = pos + 3 * i;
+        if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]))) continue;
         for (int k = 0; k < 3; ++k) {
-            lo[k] = first ? p.pos[k] : std::min(lo[k], p.pos[k]);
-            hi[k] = first ? p.pos[k] : std::max(hi[k], p.pos[k]);
+            lo[k] = first ? p[k] : std::min(lo[k], p[k]);
+            hi[k] = first ? p[k] : std::max(hi[k], p[k]);
         }
         first = false;
     }
-    double cell = (h->S.cfg.irradiance_radius > 0 ? h->S.cfg.irradiance_radius : 1.0) / 3.0;
+    M.count = nr;
+    double cell = (irradiance_radius > 0 ? irradiance_radius : 1.0) / 3.0;
     int64_t dims[3];
     for (;;) {
         double cells = 1.0;
@@ -2109,12 +2241,13 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
     M.cell = cell;
     M.inv_cell = 1.0 / cell;
     const int64_t ncells = dims[0] * dims[1] * dims[2];
-    // the cell of each photon, as the device computes it (floor((x - origin) * inv_cell)), clamped
-    std::vector<int32_t> cell_of((size_t)n), start((size_t)ncells + 1, 0);
+    // the cell of each reachable photon, as the device computes it (floor((x - origin) * inv_cell)), clamped
+    std::vector<int32_t> cell_of((size_t)n, -1), start((size_t)ncells + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
+        if (!reachable(heap_of[(size_t)i])) continue;
         int64_t c[3];
         for (int k = 0; k < 3; ++k) {
-            const double f = std::floor((ph[(size_t)i].pos[k] - M.origin[k]) * M.inv_cell);
+            const double f = std::floor((pos[3 * i + k] - M.origin[k]) * M.inv_cell);
             c[k] = std::isfinite(f) ? (int64_t)std::min(std::max(f, 0.0), (double)(dims[k] - 1)) : 0;
         }
         cell_of[(size_t)i] = (int32_t)((c[2] * dims[1] + c[1]) * dims[0] + c[0]);
@@ -2122,8 +2255,60 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
     }
     for (int64_t b = 0; b < ncells; ++b) start[(size_t)b + 1] += start[(size_t)b];
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    const size_t np = (size_t)std::max<int64_t>(nr, 1);
+    std::vector<float> pos4(np * 4, 0.0f);
+    std::vector<double> pwdir(np * 6, 0.0), kd((size_t)(n + 1) * 4, 0.0);
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t hx = heap_of[(size_t)i];
+        for (int k = 0; k < 3; ++k) kd[(size_t)(4 * hx + k)] = pos[3 * i + k];
+        kd[(size_t)(4 * hx + 3)] = (double)plane[(size_t)hx];
+        if (cell_of[(size_t)i] < 0) continue;
+        const int64_t j = fill[(size_t)cell_of[(size_t)i]]++;
+        for (int k = 0; k < 3; ++k) {
+            pos4[(size_t)(4 * j + k)] = (float)pos[3 * i + k];
+            pwdir[(size_t)(6 * j + k)] = power[3 * i + k];
+            pwdir[(size_t)(6 * j + 3 + k)] = dir[3 * i + k];
+        }
+        int32_t hb = hx;
+        std::memcpy(&pos4[(size_t)(4 * j + 3)], &hb, sizeof(hb));
+    }
+    const size_t b_pos4 = pos4.size() * sizeof(float), b_pw = pwdir.size() * sizeof(double);
+    const size_t b_start = start.size() * sizeof(int32_t), b_kd = kd.size() * sizeof(double);
+    const size_t o_kd = (b_pos4 + b_pw + b_start + 63) & ~(size_t)63;
+    FRT_HIP(hipMalloc(out_mem, o_kd + b_kd));
+    char* mem = (char*)*out_mem;
+    FRT_HIP(hipMemcpy(mem, pos4.data(), b_pos4, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4, pwdir.data(), b_pw, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4 + b_pw, start.data(), b_start, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + o_kd, kd.data(), b_kd, hipMemcpyHostToDevice));
+    M.pos4 = (const float*)mem;
+    M.pwdir = (const double*)(mem + b_pos4);
+    M.start = (const int32_t*)(mem + b_pos4 + b_pw);
+    M.kd = (const double*)(mem + o_kd);
+    return 0;
+}
+
+static int upload_photon_map(frt_scene_handle* h, int m, int64_t n, const double* pos, const double* power,
+                             const double* dir, double irradiance_radius) {
+    auto& G = h->gi;
+    hip_ignore(hipFree(G.map_mem[m]));
+    G.map_mem[m] = nullptr;
+    frt::PhotonMapDev M{};
+    if (make_photon_map(n, pos, power, dir, irradiance_radius, &G.map_mem[m], M)) return -1;
+    h->S.pmaps[m] = M;
+    G.photons[m] = (uint64_t)n;
+    return 0;
+}
+
+static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::StoredPhoton>& ph, double scale) {
+    const int64_t n = (int64_t)ph.size();
+    std::vector<double> pos((size_t)n * 3), power((size_t)n * 3), qdir((size_t)n * 3);
+    for (int64_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            pos[(size_t)(3 * i + k)] = ph[(size_t)i].pos[k];
+            power[(size_t)(3 * i + k)] = ph[(size_t)i].power[k] * scale;  // pm_scale_photon_power
+        }
     // pm_photon_dir of every photon, on the host's cores (acos / atan2 per photon)
-    std::vector<double> qdir((size_t)n * 3);
     {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(), 16,
                                                                        n / 65536 + 1}));
@@ -2135,32 +2320,7 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
             });
         for (auto& th : pool) th.join();
     }
-    const size_t np = (size_t)std::max<int64_t>(n, 1);
-    std::vector<float> pos4(np * 4, 0.0f);
-    std::vector<double> pwdir(np * 6, 0.0);
-    for (int64_t i = 0; i < n; ++i) {
-        const auto& p = ph[(size_t)i];
-        const int64_t j = fill[(size_t)cell_of[(size_t)i]]++;
-        const double* d = qdir.data() + 3 * i;
-        for (int k = 0; k < 3; ++k) {
-            pos4[(size_t)(4 * j + k)] = (float)p.pos[k];
-            pwdir[(size_t)(6 * j + k)] = p.power[k] * scale;  // pm_scale_photon_power
-            pwdir[(size_t)(6 * j + 3 + k)] = d[k];
-        }
-    }
-    const size_t b_pos4 = pos4.size() * sizeof(float), b_pw = pwdir.size() * sizeof(double);
-    const size_t bytes = b_pos4 + b_pw + start.size() * sizeof(int32_t);
-    FRT_HIP(hipMalloc(&G.map_mem[m], bytes));
-    char* mem = (char*)G.map_mem[m];
-    FRT_HIP(hipMemcpy(mem, pos4.data(), b_pos4, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4, pwdir.data(), b_pw, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4 + b_pw, start.data(), start.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    M.pos4 = (const float*)mem;
-    M.pwdir = (const double*)(mem + b_pos4);
-    M.start = (const int32_t*)(mem + b_pos4 + b_pw);
-    h->S.pmaps[m] = M;
-    G.photons[m] = (uint64_t)n;
-    return 0;
+    return upload_photon_map(h, m, n, pos.data(), power.data(), qdir.data(), h->S.cfg.irradiance_radius);
 }
 
 // trace_photons for one render seed: caustic map 0, global map 1
@@ -2263,8 +2423,11 @@ static void dump_walk_stats(frt_scene_handle* h) {
     std::fprintf(stderr, "walk prof (shadow, cycles):");
     const char* pn[8] = {"setup", "close", "xf_pop", "composite", "leaf_xf", "leaf_test", "leaf_post", "loop"};
     for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s=%llu", pn[k], c[frt::kDbgProf + k]);
-    std::fprintf(stderr, "\nestimate prof (cycles): scan=%llu select=%llu sum=%llu", c[frt::kDbgProf + 13],
-                 c[frt::kDbgProf + 14], c[frt::kDbgProf + 15]);
+    std::fprintf(stderr, "\nestimate prof (cycles): scan=%llu select=%llu sum=%llu band=%llu; queries over k=%llu "
+                 "unlisted=%llu slow_band=%llu order_check=%llu in_range_total=%llu",
+                 c[frt::kDbgProf + 13], c[frt::kDbgProf + 14], c[frt::kDbgProf + 15], c[frt::kDbgProf + 16],
+                 c[frt::kDbgProf + 17], c[frt::kDbgProf + 18], c[frt::kDbgProf + 19], c[frt::kDbgProf + 20],
+                 c[frt::kDbgProf + 21]);
     std::fprintf(stderr, "\nprepare prof (cycles):");
     const char* qn[5] = {"ray", "hits_load", "prepare", "spawn", "stores"};
     for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s=%llu", qn[k], c[frt::kDbgProf + 8 + k]);
@@ -2516,6 +2679,52 @@ int frt_render_rows(frt_scene_handle* h, const frt_frame_params* P, double* host
     if (rc) return rc;
     FRT_HIP(hipMemcpy(host_rgba, h->out_dev, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
+}
+
+// photon map test entry points (include/frt_device.h)
+int frt_pm_balance(const double* pos, int64_t n, int32_t* heap_of, int8_t* plane) {
+    if (n < 0 || n > ((int64_t)1 << 30) || (n > 0 && (!pos || !heap_of || !plane))) return fail("frt_pm_balance: bad arguments");
+    std::vector<int32_t> ho;
+    std::vector<int8_t> pl;
+    pm_balance_heap(pos, n, ho, pl);
+    std::memcpy(heap_of, ho.data(), (size_t)n * sizeof(int32_t));
+    std::memcpy(plane, pl.data(), (size_t)(n + 1) * sizeof(int8_t));
+    return 0;
+}
+
+int frt_pm_estimate(int device, const double* pos, const double* power, const double* dir, int64_t n,
+                    const double* queries, int64_t nq, double radius, int32_t k, double cone_k, double* irrad,
+                    int64_t* found) {
+    if (n < 0 || nq < 0 || k < 1 || !(radius > 0.0) || (nq > 0 && (!queries || !irrad || !found)) ||
+        (n > 0 && (!pos || !power || !dir)))
+        return fail("frt_pm_estimate: bad arguments");
+    if (nq == 0) return 0;
+    FRT_HIP(hipSetDevice(device));
+    void* mem = nullptr;
+    frt::PhotonMapDev M{};
+    double *dq = nullptr, *dirr = nullptr;
+    int64_t* dfound = nullptr;
+    int rc = make_photon_map(n, pos, power, dir, radius, &mem, M);
+    auto run = [&]() -> int {
+        FRT_HIP(hipMalloc(&dq, (size_t)nq * 6 * sizeof(double)));
+        FRT_HIP(hipMalloc(&dirr, (size_t)nq * 3 * sizeof(double)));
+        FRT_HIP(hipMalloc(&dfound, (size_t)nq * sizeof(int64_t)));
+        FRT_HIP(hipMemcpy(dq, queries, (size_t)nq * 6 * sizeof(double), hipMemcpyHostToDevice));
+        const int64_t waves_per_block = frt::kBlock / 64;
+        const int64_t blocks = (nq + waves_per_block - 1) / waves_per_block;
+        hipLaunchKernelGGL(frt::k_pm_estimate, dim3((unsigned)blocks), dim3(frt::kBlock), 0, 0, M, dq, nq, radius, (int)k,
+                           cone_k, dirr, dfound);
+        FRT_HIP(hipGetLastError());
+        FRT_HIP(hipMemcpy(irrad, dirr, (size_t)nq * 3 * sizeof(double), hipMemcpyDeviceToHost));
+        FRT_HIP(hipMemcpy(found, dfound, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost));
+        return 0;
+    };
+    if (rc == 0) rc = run();
+    hip_ignore(hipFree(dq));
+    hip_ignore(hipFree(dirr));
+    hip_ignore(hipFree(dfound));
+    hip_ignore(hipFree(mem));
+    return rc;
 }
 
 }  // extern "C"

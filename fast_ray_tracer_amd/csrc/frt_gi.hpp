@@ -49,24 +49,39 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
 }
 
 // ---- wave-cooperative estimate ----
-// pm_irradiance_estimate (pm.c:91-155) with the 64 lanes of a wave working on
-// ONE query point (wave-uniform x): the k nearest photons within max_dist (the
-// reference's max-heap in pm_locate_photons keeps exactly the k smallest
-// squared distances), cone-filtered, photons arriving from the "normal" side
-// only; zero below 8 photons, as in the reference.
+// pm_irradiance_estimate (pm.c:91-156) with the 64 lanes of a wave working on ONE query point
+// (wave-uniform x), reproducing the reference's search (pm_locate_photons, pm.c:163-252) exactly:
+//  * the photons it can reach: the host drops the heap positions whose parent is not below
+//    half_stored = n/2 - 1 (pm.c:172, 372) from the grid (frt_engine.hip upload_photon_map);
+//  * "within max_dist": the binary64 squared distance in the reference's order (p - x per axis) below
+//    max_dist^2. Binary32 distances decide it when they are farther from the radius than their error
+//    bound tol (below), the binary64 positions of the kd-tree the rest;
+//  * the selection: with at most k photons in range, all of them and dist2[0] = max_dist^2. Otherwise
+//    the first k photons found (the kd traversal, near child first, a node after its subtrees) fill
+//    the candidate array and the (k+1)-th replaces the largest of them whatever its own distance
+//    (dist2[0] is still max_dist^2 when it is tested), after which a photon enters only below the
+//    heap's maximum: the result is the k nearest in range except m, the largest of the first k found.
+//    m is one of the k nearest exactly when the traversal finds all k nearest before any other photon
+//    in range; the result is then the k nearest without the k-th plus the (k+1)-th, and dist2[0] the
+//    (k+1)-th distance, else the k-th (oracle/pm_oracle.py states both forms and checks them against
+//    each other and the reference's dumps);
+//  * the sums (pm.c:129-145) over the selected photons, the density over pi dist2[0].
+// Ties of binary64 distances (the order among equal values inside the reference's heap) are not
+// reproduced; the sums run in another order (the cone-filter weights from binary64 distances).
 //
-// Candidates come from the dense grid of PhotonMapDev (cell edge radius / 3):
-// the grid rows (y, z) within reach of the sphere, each clipped in x to the
-// sphere's chord, are concatenated and scanned 64 photons at a time
-// (coalesced binary32 positions); photons within the radius are compacted into
-// the wave's LDS list (ballot + rank), the k-th smallest distance is found by a
-// radix select over 24-bit keys of d^2 / r^2 (LDS histograms: the first digit's
-// built during the scan; when the k-th falls in a bin of at most 64 photons they
-// are ranked directly in the sum pass, else up to two more passes over the
-// list), and the cone-filtered sum is one more pass with a wave reduction. A list longer than the wave's capacity (a dense caustic) is not stored: the
-// select and sum passes then re-scan the rows. Distances are binary32 here (the
-// estimate is a statistical quantity: the reference's photon maps come from
-// drand48); the sums are binary64.
+// Candidates come from the dense grid of PhotonMapDev (cell edge radius / 3): the grid rows (y, z)
+// within reach of the sphere, each clipped in x to the sphere's chord, are concatenated and scanned 64
+// photons at a time (coalesced binary32 positions); photons within the radius are compacted into the
+// wave's LDS list (ballot + rank) with the histogram of the top byte of their 24-bit keys of
+// d^2 / r^2 (binary32). The k-th and (k+1)-th keys are found by radix selects over the keys; the
+// photons whose keys lie within the error margin of that pair ("band", usually 2-3) are ranked by
+// their binary64 distances: the k-th and (k+1)-th exact distances and the (k+1)-th's heap index. The
+// traversal order test needs no traversal: photon a comes before photon b iff a lies in b's subtree,
+// or, at their lowest common ancestor, on the side the query's near-first order takes first; with
+// b = the (k+1)-th, that side is one bit per ancestor of b (near_mask). The sum pass checks every
+// selected photon against it; only when all come first (rare) is the last of them found and every
+// other photon in range checked against it. A list longer than the wave's capacity (a dense caustic)
+// is not stored: the passes then re-scan the rows.
 constexpr int kEstCap = 1024;
 
 struct EstLds {
@@ -91,6 +106,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+__device__ __forceinline__ double readlane_dd(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 __device__ __forceinline__ float wave_max_f(float v) {
@@ -202,8 +223,64 @@ __device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, d
     }
 }
 
-// all 64 lanes call with the same x / normal; returns the photons used (the
-// reference's `found`) and the irradiance, in every lane
+// the binary64 squared distance of heap photon h in the reference's order (pm.c:188-193)
+__device__ __forceinline__ double kd_d2(const double* __restrict__ kd, int32_t h, const double* x) {
+    const double2* q = reinterpret_cast<const double2*>(kd + 4 * (int64_t)h);
+    const double2 a = q[0], b = q[1];
+    double d = a.x - x[0];
+    double d2 = d * d;
+    d = a.y - x[1];
+    d2 += d * d;
+    d = b.x - x[2];
+    d2 += d * d;
+    return d2;
+}
+
+__device__ __forceinline__ int32_t heap_of(const PhotonMapDev& M, int32_t p) {
+    return __float_as_int(M.pos4[4 * (int64_t)p + 3]);
+}
+
+// (all lanes) bit j: at the ancestor of heap node q at depth j (root 0), the query's traversal visits
+// the right child first (pm.c:173-183: dist1 = x[plane] - p[plane] > 0)
+__device__ __forceinline__ unsigned near_mask(const double* __restrict__ kd, int32_t q, const double* x) {
+    const int dq = 31 - __clz(q), lane = est_lane();
+    bool right = false;
+    if (lane < dq) {
+        const double* c = kd + 4 * (int64_t)(q >> (dq - lane));
+        const int ax = (int)c[3];
+        right = x[ax] - c[ax] > 0.0;
+    }
+    return (unsigned)__ballot(right);
+}
+
+// heap node a (!= q) is found before node q by the query's traversal; qmask = near_mask(q)
+__device__ __forceinline__ bool found_before(int32_t a, int32_t q, unsigned qmask) {
+    const int da = 31 - __clz(a), dq = 31 - __clz(q);
+    if (da > dq && (a >> (da - dq)) == q) return true;   // in q's subtree: before q
+    if (dq > da && (q >> (dq - da)) == a) return false;  // an ancestor of q: after it
+    const int m = min(da, dq);
+    const int32_t a2 = a >> (da - m), q2 = q >> (dq - m);
+    const int up = 32 - __clz(a2 ^ q2);  // levels from depth m up to the common ancestor
+    return ((a2 >> (up - 1)) & 1) == (int)((qmask >> (m - up)) & 1u);
+}
+
+// the same for any pair, the common ancestor's split read from the kd-tree (the rare full check)
+__device__ __forceinline__ bool found_before_any(const double* __restrict__ kd, int32_t a, int32_t b, const double* x) {
+    const int da = 31 - __clz(a), db = 31 - __clz(b);
+    if (da > db && (a >> (da - db)) == b) return true;
+    if (db > da && (b >> (db - da)) == a) return false;
+    const int m = min(da, db);
+    const int32_t a2 = a >> (da - m), b2 = b >> (db - m);
+    const int up = 32 - __clz(a2 ^ b2);
+    const double* c = kd + 4 * (int64_t)(a2 >> up);
+    const int ax = (int)c[3];
+    return ((a2 >> (up - 1)) & 1) == (x[ax] - c[ax] > 0.0 ? 1 : 0);
+}
+
+__device__ __forceinline__ unsigned wave_and(bool v) { return __ballot(!v) == 0ull ? 1u : 0u; }
+
+// all 64 lanes call with the same x / normal; returns the photons used (the reference's `found`) and
+// the irradiance, in every lane
 #ifdef FRT_WALK_PROF
 #define EST_STAMP(k)                                                                      \
     do {                                                                                  \
@@ -211,8 +288,13 @@ __device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, d
         if (lane == 0 && prof) atomicAdd(prof + (k), t1_ - est_t0);                      \
         est_t0 = t1_;                                                                     \
     } while (0)
+#define EST_COUNT(k, v)                                   \
+    do {                                                  \
+        if (lane == 0 && prof) atomicAdd(prof + (k), (v)); \
+    } while (0)
 #else
 #define EST_STAMP(k)
+#define EST_COUNT(k, v)
 #endif
 __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
                                                    double max_dist, int k, double cone_k, double* irrad,
@@ -224,28 +306,50 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
 #endif
     const int lane = est_lane();
     const double r2 = max_dist * max_dist;
-    const float r2f = (float)r2, inv_r2 = (float)(1.0 / r2);
-    // pass 1: the photons within the radius, compacted into the LDS list in scan order, and the
-    // histogram of their keys' top byte (the radix select's first digit)
+    // error bound of a binary32 squared distance against the reference's binary64 one, for points
+    // within reach of the radius: each difference within eb = 1.01u (2A + 2r) (A = max|x| + r: the two
+    // positions' roundings and the subtraction's), the squares and sums adding 2 |d| eb + eb^2 and 3u d^2
+    const double A = fmax(fmax(fabs(x[0]), fabs(x[1])), fabs(x[2])) + max_dist;
+    const double eb = 1.01 * 0x1p-24 * (2.0 * A + 2.0 * max_dist);
+    const double tol = 1.02 * (4.0 * max_dist * eb + 3.0 * eb * eb + 4.0 * 0x1p-24 * r2);
+    const float lo_thr = __double2float_rd(r2 - tol), hi_thr = __double2float_ru(r2 + tol);
+    const float inv_r2 = (float)(1.0 / r2);
+    // keys closer than dk may belong to photons whose binary64 order differs from their keys' order
+    // (2 tol, the key's own rounding (3u relative) and its truncation)
+    const unsigned dk = (unsigned)ceil((2.0 * tol + 8.0 * 0x1p-24 * r2) * (16777216.0 / r2)) + 3u;
+    // within the radius, exactly: binary32 away from it, binary64 near it (uniform control flow)
+    auto in_range = [&](int32_t p, bool cand, float d2) {
+        bool in = cand && d2 < lo_thr;
+        const bool unc = cand && !in;
+        if (__ballot(unc)) {
+            if (unc) in = kd_d2(M.kd, heap_of(M, p), x) < r2;
+        }
+        return in;
+    };
+    // pass 1: the photons within the radius into the LDS list in scan order, and the histogram of their
+    // keys' top byte (the radix selects' first digit)
     for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
     __builtin_amdgcn_wave_barrier();
     unsigned total = 0;
-    wave_scan_cells(M, x, max_dist, r2f, [&](int32_t p, bool in, float d2) {
+    wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) {
+        const bool in = in_range(p, cand, d2);
         const unsigned long long m = __ballot(in);
         if (in) {
             const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
-            if (at < L.cap) {
-                L.ent[at] = make_uint2(__float_as_uint(d2), (unsigned)p);
-            }
+            if (at < L.cap) L.ent[at] = make_uint2(__float_as_uint(d2), (unsigned)p);
             atomicAdd(&L.hist[est_key(d2, inv_r2) >> 16], 1u);
         }
         total += (unsigned)__popcll(m);
     });
+    __builtin_amdgcn_wave_barrier();
     EST_STAMP(0);
     const unsigned found = total < (unsigned)k ? total : (unsigned)k;
     if (found < 8) return found;
     const bool listed = total <= L.cap;
-    // every pass visits the in-range photons in the same order: from the list, or a re-scan
+    EST_COUNT(4, total > (unsigned)k ? 1ull : 0ull);
+    EST_COUNT(5, listed ? 0ull : 1ull);
+    EST_COUNT(8, (unsigned long long)total);
+    // every pass visits the photons in range in the same order: from the list, or a re-scan
     auto visit = [&](auto&& fn) {
         if (listed) {
             for (unsigned base = 0; base < total; base += 64) {
@@ -255,83 +359,9 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
                 fn((int32_t)e.y, in, __uint_as_float(e.x));
             }
         } else {
-            wave_scan_cells(M, x, max_dist, r2f, fn);
+            wave_scan_cells(M, x, max_dist, hi_thr,
+                            [&](int32_t p, bool cand, float d2) { fn(p, in_range(p, cand, d2), d2); });
         }
-    };
-    // the k-th smallest key: radix select, 8 bits per pass
-    unsigned prefix = 0, mask = 0, need = found;
-    bool resolved = total <= (unsigned)k;  // every photon in range is used
-    bool few_ties = false;  // the k-th lies among <= 64 photons of one bin: ranked directly in the sum pass
-    for (int shift = 16; shift >= 0 && !resolved; shift -= 8) {
-        if (shift != 16) {  // (the first digit's histogram came with pass 1)
-            for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
-            __builtin_amdgcn_wave_barrier();
-            visit([&](int32_t, bool in, float d2) {
-                const unsigned key = est_key(d2, inv_r2);
-                if (in && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
-            });
-        }
-        __builtin_amdgcn_wave_barrier();
-        unsigned h4[4], local = 0;
-        for (int j = 0; j < 4; ++j) {
-            h4[j] = L.hist[4 * lane + j];
-            local += h4[j];
-        }
-        const unsigned incl = wave_incl_scan(local);
-        const unsigned long long hit = __ballot(incl >= need);
-        const int owner = __builtin_ctzll(hit);
-        // the owner lane walks its four bins
-        unsigned below = incl - local;
-        int bin = 4 * lane + 3;
-        unsigned cnt = h4[3];
-        for (int j = 0; j < 4; ++j) {
-            if (below + h4[j] >= need) {
-                bin = 4 * lane + j;
-                cnt = h4[j];
-                break;
-            }
-            below += h4[j];
-        }
-        bin = __builtin_amdgcn_readlane(bin, owner);
-        cnt = __builtin_amdgcn_readlane(cnt, owner);
-        below = __builtin_amdgcn_readlane(below, owner);
-        need -= below;
-        prefix |= (unsigned)bin << shift;
-        mask |= 255u << shift;
-        resolved = cnt == need;
-        if (!resolved && cnt <= 64u) {
-            few_ties = true;
-            break;
-        }
-    }
-    EST_STAMP(1);
-    // sum pass (pm.c:125-145): keys below the k-th are in; at the k-th key the first `need` met
-    const double cone_r = cone_k * max_dist;
-    double acc[3] = {0.0, 0.0, 0.0};
-    float dmax = 0.0f;
-    unsigned ties = 0;
-    const bool all = total <= (unsigned)k;
-    // few_ties: the bin's photons (the "ties" at the selected prefix) are set aside in L.hist
-    // (index, d^2, key at scan position r < 64) and the `need` smallest by (key, scan order) taken
-    // after the pass: the same photons as a further select pass would keep
-    auto decide = [&](int32_t p, bool in, float d2) {
-        const unsigned key = est_key(d2, inv_r2);
-        const bool lower = in && (all || (key & mask) < prefix);
-        const bool tie = in && !all && (key & mask) == prefix;
-        const unsigned long long tm = __ballot(tie);
-        const unsigned r = ties + (unsigned)__popcll(tm & ((1ull << lane) - 1));
-        bool take = lower;
-        if (few_ties) {
-            if (tie) {
-                L.hist[r] = (unsigned)p;
-                L.hist[64 + r] = __float_as_uint(d2);
-                L.hist[128 + r] = key;
-            }
-        } else {
-            take = take || (tie && (resolved || r < need));
-        }
-        ties += (unsigned)__popcll(tm);
-        return take;
     };
     // one 48-byte record per photon: power x, y, z, direction x, y, z
     auto record = [&](int32_t p, double2* r) {
@@ -340,63 +370,290 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         r[1] = rec[1];
         r[2] = rec[2];
     };
-    auto accumulate = [&](float d2, const double2* r) {
-        dmax = fmaxf(dmax, d2);
-        const double weight = 1.0 - (double)sqrtf(d2) / cone_r;
+    const double cone_r = cone_k * max_dist;
+    double acc[3] = {0.0, 0.0, 0.0};
+    auto accumulate = [&](double dp, const double2* r) {
+        const double weight = 1.0 - dp / cone_r;
         if ((r[1].y * normal[0] + r[2].x * normal[1] + r[2].y * normal[2]) < 0.0) {
             acc[0] += r[0].x * weight;
             acc[1] += r[0].y * weight;
             acc[2] += r[1].x * weight;
         }
     };
-    if (listed) {  // two chunks per step: both record loads in flight together
-        for (unsigned base = 0; base < total; base += 128) {
-            const unsigned ia = base + (unsigned)lane, ib = ia + 64u;
-            const bool ina = ia < total, inb = ib < total;
-            const uint2 ea = ina ? L.ent[ia] : make_uint2(0u, 0u), eb = inb ? L.ent[ib] : make_uint2(0u, 0u);
-            const int32_t pa = (int32_t)ea.y, pb = (int32_t)eb.y;
-            const float d2a = __uint_as_float(ea.x), d2b = __uint_as_float(eb.x);
-            const bool ta = decide(pa, ina, d2a), tb = decide(pb, inb, d2b);
-            double2 ra[3], rb[3];
-            if (ta) record(pa, ra);
-            if (tb) record(pb, rb);
-            if (ta) accumulate(d2a, ra);
-            if (tb) accumulate(d2b, rb);
-        }
-    } else {
-        wave_scan_cells(M, x, max_dist, r2f, [&](int32_t p, bool in, float d2) {
-            if (decide(p, in, d2)) {
+    auto finish = [&](double d0) {
+        for (int j = 0; j < 3; ++j) irrad[j] = wave_sum_d(acc[j]);
+        // np.dist2[0] (pm.c:147)
+        const double tmp = 1.0 / ((1.0 - 2.0 / (3.0 * cone_k)) * (kPi * d0));
+        irrad[0] *= tmp;
+        irrad[1] *= tmp;
+        irrad[2] *= tmp;
+    };
+    if (total <= (unsigned)k) {  // every photon in range: no heap, dist2[0] = max_dist^2
+        visit([&](int32_t p, bool in, float d2) {
+            if (in) {
                 double2 r[3];
                 record(p, r);
-                accumulate(d2, r);
+                accumulate(sqrt(kd_d2(M.kd, heap_of(M, p), x)), r);
+            }
+        });
+        finish(r2);
+        EST_STAMP(2);
+        return found;
+    }
+    // ---- the k-th and (k+1)-th keys: radix selects, 8 bits per digit ----
+    unsigned h4[4];  // the first digit's histogram, kept for the second select
+    for (int j = 0; j < 4; ++j) h4[j] = L.hist[4 * lane + j];
+    auto select = [&](unsigned need, unsigned& lo, unsigned& hi) {
+        unsigned prefix = 0, mask = 0;
+        for (int shift = 16; shift >= 0; shift -= 8) {
+            unsigned c4[4], local = 0;
+            if (shift == 16) {
+                for (int j = 0; j < 4; ++j) c4[j] = h4[j];
+            } else {
+                for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+                __builtin_amdgcn_wave_barrier();
+                visit([&](int32_t, bool in, float d2) {
+                    const unsigned key = est_key(d2, inv_r2);
+                    if (in && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
+                });
+                __builtin_amdgcn_wave_barrier();
+                for (int j = 0; j < 4; ++j) c4[j] = L.hist[4 * lane + j];
+            }
+            for (int j = 0; j < 4; ++j) local += c4[j];
+            const unsigned incl = wave_incl_scan(local);
+            const int owner = __builtin_ctzll(__ballot(incl >= need));
+            unsigned below = incl - local, cnt = c4[3];
+            int bin = 4 * lane + 3;
+            for (int j = 0; j < 4; ++j) {
+                if (below + c4[j] >= need) {
+                    bin = 4 * lane + j;
+                    cnt = c4[j];
+                    break;
+                }
+                below += c4[j];
+            }
+            bin = __builtin_amdgcn_readlane(bin, owner);
+            cnt = __builtin_amdgcn_readlane(cnt, owner);
+            below = __builtin_amdgcn_readlane(below, owner);
+            need -= below;
+            prefix |= (unsigned)bin << shift;
+            mask |= 255u << shift;
+            if (cnt <= 64u) break;  // few enough: the band ranks them
+        }
+        lo = prefix;
+        hi = prefix | (~mask & 0xFFFFFFu);
+    };
+    unsigned klo, khi, k1lo, k1hi;
+    select((unsigned)k, klo, khi);
+    select((unsigned)k + 1u, k1lo, k1hi);
+    const unsigned blo = klo > dk ? klo - dk : 0u, bhi = min(k1hi + dk, 0xFFFFFFu);
+    EST_STAMP(1);
+    // ---- the band: ranked by binary64 distance ----
+    // pass B: photons with keys in [blo, bhi] set aside (up to 64, in L.hist), the certain ones counted
+    unsigned c_in = 0, nb = 0;
+    visit([&](int32_t p, bool in, float d2) {
+        const unsigned key = est_key(d2, inv_r2);
+        const bool band = in && key >= blo && key <= bhi;
+        const unsigned long long bm = __ballot(band);
+        if (band) {
+            const unsigned at = nb + (unsigned)__popcll(bm & ((1ull << lane) - 1));
+            if (at < 64u) L.hist[at] = (unsigned)p;
+        }
+        nb += (unsigned)__popcll(bm);
+        c_in += (unsigned)__popcll(__ballot(in && key < blo));
+    });
+    __builtin_amdgcn_wave_barrier();
+    const unsigned need = (unsigned)k - c_in;  // band ranks of the k-th (need - 1) and the (k+1)-th (need)
+    double vk = r2, vk1 = r2;
+    int32_t R = 1;
+    bool mine_band = false;  // this lane holds a band photon (fast path)
+    int32_t bp = 0, bh = 1;
+    double bv = 0.0;
+    unsigned brank = 0;
+    const bool fast = nb <= 64u && need >= 1u && need + 1u <= nb;
+    if (fast) {
+        mine_band = (unsigned)lane < nb;
+        if (mine_band) {
+            bp = (int32_t)L.hist[lane];
+            bh = heap_of(M, bp);
+            bv = kd_d2(M.kd, bh, x);
+        }
+        for (unsigned j = 0; j < nb; ++j) {
+            const double vj = readlane_dd(bv, (int)j);
+            brank += (vj < bv || (vj == bv && j < (unsigned)lane)) ? 1u : 0u;
+        }
+        const int ok = __builtin_ctzll(__ballot(mine_band && brank == need - 1u));
+        const int ok1 = __builtin_ctzll(__ballot(mine_band && brank == need));
+        vk = readlane_dd(bv, ok);
+        vk1 = readlane_dd(bv, ok1);
+        R = __builtin_amdgcn_readlane(bh, ok1);
+    } else {
+        EST_COUNT(6, 1ull);
+        // many photons in the band (a dense caustic): exact radix selects over the band's binary64
+        // distances (their bit patterns order like the values), passes over the list
+        auto exact_rank = [&](unsigned rk) {
+            unsigned long long prefix = 0, mask = 0;
+            for (int shift = 56; shift >= 0; shift -= 8) {
+                for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+                __builtin_amdgcn_wave_barrier();
+                visit([&](int32_t p, bool in, float d2) {
+                    const unsigned key = est_key(d2, inv_r2);
+                    const bool band = in && key >= blo && key <= bhi;
+                    if (band) {
+                        const unsigned long long b = (unsigned long long)__double_as_longlong(kd_d2(M.kd, heap_of(M, p), x));
+                        if ((b & mask) == prefix) atomicAdd(&L.hist[(unsigned)((b >> shift) & 255ull)], 1u);
+                    }
+                });
+                __builtin_amdgcn_wave_barrier();
+                unsigned c4[4], local = 0;
+                for (int j = 0; j < 4; ++j) {
+                    c4[j] = L.hist[4 * lane + j];
+                    local += c4[j];
+                }
+                const unsigned incl = wave_incl_scan(local);
+                const int owner = __builtin_ctzll(__ballot(incl >= rk));
+                unsigned below = incl - local;
+                int bin = 4 * lane + 3;
+                for (int j = 0; j < 4; ++j) {
+                    if (below + c4[j] >= rk) {
+                        bin = 4 * lane + j;
+                        break;
+                    }
+                    below += c4[j];
+                }
+                bin = __builtin_amdgcn_readlane(bin, owner);
+                below = __builtin_amdgcn_readlane(below, owner);
+                rk -= below;
+                prefix |= (unsigned long long)bin << shift;
+                mask |= 255ull << shift;
+            }
+            return __longlong_as_double((long long)prefix);
+        };
+        vk = exact_rank(need);
+        vk1 = exact_rank(need + 1u);
+        int32_t rh = 0;
+        visit([&](int32_t p, bool in, float d2) {  // the (k+1)-th's heap index (first of equal distances)
+            const unsigned key = est_key(d2, inv_r2);
+            int32_t hx = 0;
+            if (in && key >= blo && key <= bhi) {
+                hx = heap_of(M, p);
+                if (kd_d2(M.kd, hx, x) != vk1) hx = 0;
+            }
+            const unsigned long long hm = __ballot(hx != 0);
+            if (rh == 0 && hm) rh = __builtin_amdgcn_readlane(hx, __builtin_ctzll(hm));
+        });
+        R = rh != 0 ? rh : 1;
+    }
+    EST_STAMP(3);
+    // ---- sum pass over the k nearest, checking that each comes before the (k+1)-th ----
+    const unsigned qmask = near_mask(M.kd, R, x);
+    bool before_all = true;
+    unsigned below_k = 0;  // (slow path) band photons strictly nearer than the k-th
+    auto band_member = [&](double v) { return v <= vk; };
+    visit([&](int32_t p, bool in, float d2) {
+        const unsigned key = est_key(d2, inv_r2);
+        const bool certain = in && key < blo;
+        const bool band = in && key >= blo && key <= bhi && !fast;
+        if (certain) {
+            const int32_t hx = heap_of(M, p);
+            double2 r[3];
+            record(p, r);
+            accumulate(sqrt(kd_d2(M.kd, hx, x)), r);
+            before_all = before_all && found_before(hx, R, qmask);
+        }
+        if (__ballot(band)) {  // (slow path) band photons: membership by their binary64 distance
+            bool nearer = false;
+            if (band) {
+                const int32_t hx = heap_of(M, p);
+                const double v = kd_d2(M.kd, hx, x);
+                nearer = v < vk;
+                if (nearer) {  // those at the k-th's and the (k+1)-th's distance are added after the check
+                    double2 r[3];
+                    record(p, r);
+                    accumulate(sqrt(v), r);
+                }
+                if (band_member(v) && hx != R) before_all = before_all && found_before(hx, R, qmask);
+            }
+            below_k += (unsigned)__popcll(__ballot(nearer));
+        }
+    });
+    if (fast && mine_band && brank < need) before_all = before_all && found_before(bh, R, qmask);
+    bool quirk = false;
+    if (wave_and(before_all)) {
+        // every one of the k nearest precedes the (k+1)-th: the traversal may have found them first.
+        // The last of them in traversal order, then every other photon in range against it.
+        EST_COUNT(7, 1ull);
+        int32_t last = 0;
+        auto consider = [&](int32_t hx) {
+            if (last == 0 || found_before_any(M.kd, last, hx, x)) last = hx;
+        };
+        visit([&](int32_t p, bool in, float d2) {
+            const unsigned key = est_key(d2, inv_r2);
+            if (in && key < blo) consider(heap_of(M, p));
+            if (in && key >= blo && key <= bhi && !fast) {
+                const int32_t hx = heap_of(M, p);
+                if (band_member(kd_d2(M.kd, hx, x))) consider(hx);
+            }
+        });
+        if (fast && mine_band && brank < need) consider(bh);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int32_t other = __shfl_xor(last, o, 64);
+            if (other != 0) consider(other);
+        }
+        const int32_t Lh = __builtin_amdgcn_readlane(last, 0);
+        const unsigned lmask = near_mask(M.kd, Lh, x);
+        bool after = true;
+        visit([&](int32_t p, bool in, float d2) {
+            const unsigned key = est_key(d2, inv_r2);
+            bool other = in && key > bhi;
+            int32_t hx = 0;
+            if (in && key >= blo && key <= bhi && !fast) {
+                hx = heap_of(M, p);
+                other = !band_member(kd_d2(M.kd, hx, x));
+            }
+            if (other) after = after && !found_before(hx != 0 ? hx : heap_of(M, p), Lh, lmask);
+        });
+        if (fast && mine_band && brank >= need) after = after && !found_before(bh, Lh, lmask);
+        quirk = wave_and(after);
+    }
+    // the band's selected photons: ranks below need (the k-th excluded and the (k+1)-th included when
+    // the traversal found the k nearest first)
+    if (fast) {
+        if (mine_band && (quirk ? (brank + 1u < need || brank == need) : brank < need)) {
+            double2 r[3];
+            record(bp, r);
+            accumulate(sqrt(bv), r);
+        }
+    } else {
+        // slow path: photons at the k-th's distance up to rank k (rank k - 1 when the (k+1)-th replaces
+        // the k-th), then the (k+1)-th (ties: the first ones visited)
+        unsigned take_k = need - below_k, take_k1 = 0;
+        if (quirk && vk1 != vk) {  // (at equal distances the count at vk stays)
+            take_k -= 1;
+            take_k1 = 1;
+        }
+        visit([&](int32_t p, bool in, float d2) {
+            const unsigned key = est_key(d2, inv_r2);
+            const bool band = in && key >= blo && key <= bhi;
+            if (__ballot(band)) {
+                double v = -1.0;
+                if (band) v = kd_d2(M.kd, heap_of(M, p), x);
+                const bool ek = band && v == vk, ek1 = band && v == vk1 && vk1 != vk;
+                const unsigned long long below = (1ull << lane) - 1;
+                const unsigned long long mk = __ballot(ek), mk1 = __ballot(ek1);
+                if ((ek && (unsigned)__popcll(mk & below) < take_k) || (ek1 && (unsigned)__popcll(mk1 & below) < take_k1)) {
+                    double2 r[3];
+                    record(p, r);
+                    accumulate(sqrt(v), r);
+                }
+                take_k -= min(take_k, (unsigned)__popcll(mk));
+                take_k1 -= min(take_k1, (unsigned)__popcll(mk1));
             }
         });
     }
-    if (few_ties) {
-        __builtin_amdgcn_wave_barrier();
-        const bool mine = (unsigned)lane < ties;
-        const unsigned kl = mine ? L.hist[128 + lane] : 0xffffffffu;
-        unsigned rank = 0;
-        for (unsigned m = 0; m < ties; ++m) {
-            const unsigned km = (unsigned)__builtin_amdgcn_readlane((int)kl, (int)m);
-            rank += (km < kl || (km == kl && m < (unsigned)lane)) ? 1u : 0u;
-        }
-        if (mine && rank < need) {
-            const float d2 = __uint_as_float(L.hist[64 + lane]);
-            double2 r[3];
-            record((int32_t)L.hist[lane], r);
-            accumulate(d2, r);
-        }
-    }
-    for (int j = 0; j < 3; ++j) irrad[j] = wave_sum_d(acc[j]);
-    dmax = wave_max_f(dmax);
+    finish(quirk ? vk1 : vk);
     EST_STAMP(2);
-    // np.dist2[0]: max_dist^2 until the heap filled, then its largest entry (pm.c:244)
-    const double d0 = all ? r2 : (double)dmax;
-    const double tmp = 1.0 / ((1.0 - 2.0 / (3.0 * cone_k)) * (kPi * d0));
-    irrad[0] *= tmp;
-    irrad[1] *= tmp;
-    irrad[2] *= tmp;
     return found;
 }
 

@@ -94,11 +94,13 @@ __device__ __forceinline__ void frame_cache(const Ray& r, FrameCache& c) {
 // (x fastest, so a row of cells is one contiguous photon range), built on the
 // host after tracing
 struct PhotonMapDev {
-    const float* pos4;    // 4 per photon: binary32 x, y, z, 0 (the estimate's candidate scan)
+    const float* pos4;    // 4 per photon: binary32 x, y, z, heap index (int bits) (the estimate's candidate scan)
     const double* pwdir;  // 6 per photon: power (scaled by 1 / photon_count), then pm_photon_dir of
                           // the stored theta / phi bytes (pm.c:80-88)
     const int32_t* start; // cell -> first photon, cells + 1 entries
-    int64_t count;
+    const double* kd;     // 4 per heap index (pm_balance's kd-tree, frt_engine.hip pm_balance_heap): binary64
+                          // x, y, z and the split plane; .w of pos4 holds each photon's heap index
+    int64_t count;        // photons in the grid (those the reference's search reaches)
     int32_t dims[3];      // cells per axis
     int32_t pad;
     double origin[3];     // grid origin (the photons' lower bounding-box corner)
@@ -137,7 +139,7 @@ enum FeatureBits : int { kFeatCsg = 1, kFeatTorus = 2 };
 
 // FRT_WALK_STATS builds: 16 global counters + per node (first kDbgNodes) {wave visits, active lanes} x 2 walks
 constexpr int kDbgNodes = 64;
-constexpr int kDbgSlots = 16 + 4 * kDbgNodes + 16;
+constexpr int kDbgSlots = 16 + 4 * kDbgNodes + 32;
 constexpr int kDbgProf = 16 + 4 * kDbgNodes;  // FRT_WALK_PROF builds: s_memtime cycles per walk region (shadow)
 
 #ifdef FRT_WALK_PROF

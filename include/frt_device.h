@@ -249,6 +249,20 @@ void frt_scene_release(frt_scene_handle *h);
  * the compiler log, `src` (may be NULL) the generated HIP source. */
 int frt_jit_check(const frt_scene *scene, char *log, size_t log_cap, char *src, size_t src_cap);
 
+/* Photon map entry points (parity tests; no scene needed).
+ * frt_pm_balance replaces pm_balance (reference src/libs/photon_map/pm.c:329-494): the balanced
+ * kd-tree of n photons given in the reference's storage order (pos: 3 doubles each); heap_of[i] = the
+ * heap index (1..n) of photon i, plane[h] (n + 1 entries) = the split axis of heap node h. Host only.
+ * frt_pm_estimate replaces pm_irradiance_estimate (pm.c:91-156, with pm_locate_photons pm.c:163-252)
+ * over one map balanced as above: nq queries (pos[3], normal[3] each) on `device`; irrad receives 3
+ * doubles per query (before lighting_gi's scaling), found the photons used. pos / power / dir: 3
+ * doubles per photon in storage order, power already scaled (pm_scale_photon_power), dir = pm_photon_dir
+ * of the photon's theta / phi. */
+int frt_pm_balance(const double *pos, int64_t n, int32_t *heap_of, int8_t *plane);
+int frt_pm_estimate(int device, const double *pos, const double *power, const double *dir, int64_t n,
+                    const double *queries, int64_t nq, double radius, int32_t k, double cone_k,
+                    double *irrad, int64_t *found);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,7 +9,8 @@
 # codegen output (yaml_parser.py scene.yml > main.c) + oracle/ref_harness.c,
 # with main.c's render_multi / trace_photons calls routed through the harness so the
 # raw canvas and the render_multi wall time can be captured
-# (FRT_REF_CANVAS=<file>, FRT_REF_STATS=<file>). Used to pin the CPU oracle
+# (FRT_REF_CANVAS=<file>, FRT_REF_STATS=<file>), and pm_balance wrapped (--wrap) so the photon
+# maps and pm_irradiance_estimate results can be dumped (FRT_REF_PM_*). Used to pin the CPU oracle
 # (tests/golden/make_golden.py) and as bench.py's cpu_baseline ("reference").
 #
 # Container workarounds recorded in SURVEY.md section 8(c): the reference
@@ -32,7 +33,7 @@ fi
 
 CC=${CC:-gcc}
 CFLAGS=(-std=c11 -O2 -w -D_DEFAULT_SOURCE -I/opt/conda/include)
-LDFLAGS=(-L/opt/conda/lib -Wl,-rpath,/opt/conda/lib -lpng16 -lz -lm -lpthread)
+LDFLAGS=(-L/opt/conda/lib -Wl,-rpath,/opt/conda/lib -Wl,--wrap=pm_balance -lpng16 -lz -lm -lpthread)
 
 mkdir -p "$OUT/obj" "$OUT/bin"
 

@@ -7,13 +7,86 @@
  */
 #include <stdio.h>
 #include <stdlib.h>
+#include <stdint.h>
 #include <time.h>
 
 #include "src/renderer/renderer.h"
 
 #include "src/renderer/photon_tracer.h"
+#include "src/libs/photon_map/pm.h"
 
 static int g_traced_photons = 0;
+
+/* ---- photon-map fixtures (FRT_REF_PM_DUMP=<prefix>) ----
+ * The build links with -Wl,--wrap=pm_balance, so trace_photons' pm_balance calls (reference
+ * photon_tracer.c:254-256, pm.c:329) come here: map m's photons are written before balancing
+ * (<prefix>_<m>_stored.bin: the stored order) and after (<prefix>_<m>_kd.bin: the balanced kd-tree,
+ * heap index 1..n). Record per photon: pos[3], power[3] (doubles), theta, phi, plane (int32 each).
+ * FRT_REF_PM_QUERIES=<file> (int32 count, then per query: int32 map, double pos[3], double normal[3])
+ * and FRT_REF_PM_OUT=<file>: after trace_photons, pm_irradiance_estimate (pm.c:91) of every query with
+ * the scene's radius / photon count / cone-filter k; per query: double irrad[3], int64 found. */
+void __real_pm_balance(PhotonMap *pm);
+static int g_balance_calls = 0;
+
+static void
+dump_photons(const PhotonMap *pm, const char *prefix, int m, const char *what)
+{
+    char path[1024];
+    snprintf(path, sizeof(path), "%s_%d_%s.bin", prefix, m, what);
+    FILE *f = fopen(path, "wb");
+    if (f == NULL)
+        return;
+    long n = pm->stored_photons;
+    fwrite(&n, sizeof(n), 1, f);
+    for (long i = 1; i <= n; ++i) {
+        const Photon *p = pm->photons + i;
+        int32_t b[3] = {p->theta, p->phi, p->plane};
+        fwrite(p->pos, sizeof(double), 3, f);
+        fwrite(p->power, sizeof(double), 3, f);
+        fwrite(b, sizeof(int32_t), 3, f);
+    }
+    fclose(f);
+}
+
+void
+__wrap_pm_balance(PhotonMap *pm)
+{
+    const char *prefix = getenv("FRT_REF_PM_DUMP");
+    const int m = g_balance_calls++;
+    if (prefix != NULL)
+        dump_photons(pm, prefix, m, "stored");
+    __real_pm_balance(pm);
+    if (prefix != NULL)
+        dump_photons(pm, prefix, m, "kd");
+}
+
+static void
+run_queries(const World w)
+{
+    const char *qpath = getenv("FRT_REF_PM_QUERIES"), *opath = getenv("FRT_REF_PM_OUT");
+    if (qpath == NULL || opath == NULL)
+        return;
+    FILE *q = fopen(qpath, "rb"), *o = fopen(opath, "wb");
+    if (q == NULL || o == NULL)
+        return;
+    int32_t n = 0;
+    if (fread(&n, sizeof(n), 1, q) != 1)
+        n = 0;
+    const double radius = w->global_config->illumination.gi.irradiance_estimate_radius;
+    const int num = (int)w->global_config->illumination.gi.irradiance_estimate_num;
+    const double cone = w->global_config->illumination.gi.irradiance_estimate_cone_filter_k;
+    for (int32_t i = 0; i < n; ++i) {
+        int32_t m;
+        double pos[3], nrm[3], irrad[3];
+        if (fread(&m, sizeof(m), 1, q) != 1 || fread(pos, sizeof(double), 3, q) != 3 || fread(nrm, sizeof(double), 3, q) != 3)
+            break;
+        int64_t found = pm_irradiance_estimate(w->photon_maps + m, irrad, pos, nrm, radius, num, cone);
+        fwrite(irrad, sizeof(double), 3, o);
+        fwrite(&found, sizeof(found), 1, o);
+    }
+    fclose(q);
+    fclose(o);
+}
 
 static void
 reseed_from_env(unsigned long long salt)
@@ -37,6 +110,7 @@ frt_ref_trace_photons(const World w, size_t num_maps, bool populate_caustic_map,
     reseed_from_env(0);
     g_traced_photons = 1;
     trace_photons(w, num_maps, populate_caustic_map, populate_global_map);
+    run_queries(w);
 }
 
 Canvas

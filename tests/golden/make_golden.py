@@ -120,6 +120,23 @@ SCENES = {
     # BASELINE configs[4]: the shipped GI configuration (1M photons, 8x8 final gather) at 1920x1080x64
     "cornell_gi_1920x1080_8x8": ("scenes/cornell_box/cornell_box.yml",
                                  {"size": (1920, 1080), "steps": (8, 8), "no_golden": True}),
+    # GI statistical goldens at 64x64 (round 2: more power than the 24 / 32 px ones)
+    "cornell_gi_64": ("scenes/cornell_box/cornell_box.yml",
+                      {"size": (64, 64), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS, "gi": {}}),
+    "cornell_gi_visualize_64": ("scenes/cornell_box/cornell_box.yml",
+                                {"size": (64, 64), "steps": (2, 2), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS,
+                                 "ill": {"visualize-photon-map": True},
+                                 "gi": {"usteps": 2, "vsteps": 2, "photon-count": 200000}}),
+    "cornell_caustics_64": ("scenes/cornell_box/cornell_box.yml",
+                            {"size": (64, 64), "steps": (2, 2), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS,
+                             "gi": {"include-caustics": True, "include-final-gather": False,
+                                    "photon-count": 100000}}),
+    # photon-map fixture scene (tests/golden/make_pm_fixture.py): both maps at 10k photons, single thread
+    "pm_cornell_10k": ("scenes/cornell_box/cornell_box.yml",
+                       {"size": (4, 4), "steps": (1, 1), "threads": 1, "no_golden": True,
+                        "gi": {"photon-count": 10000, "include-caustics": True, "include-final-gather": True,
+                               "irradiance-estimate-num": 50, "irradiance-estimate-radius": 0.3,
+                               "irradiance-estimate-cone-filter-k": 1.1}}),
     # cfg4 stand-in (bounding_boxes: 6 dragons, BVH) at its 4x4 CMJ grid, small frame
     "bounding_boxes_100x125_4x4": ("scenes/bounding_boxes/bounding_boxes.yml",
                                    {"size": (100, 125), "steps": (4, 4)}),
