@@ -810,10 +810,11 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
 }
 
 // the wave's LDS for wave_irradiance_estimate (frt_gi.hpp); blocks of kBlock threads
-#define FRT_EST_LDS(name, cap)                                               \
-    __shared__ uint2 name##_ent[kBlock / 64][cap];                           \
-    __shared__ unsigned name##_hist[kBlock / 64][256];                       \
-    const EstLds name{name##_ent[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6],                          \
+#define FRT_EST_LDS(name, cap)                                                                            \
+    __shared__ uint2 name##_ent[kBlock / 64][cap];                                                        \
+    __shared__ unsigned name##_hist[kBlock / 64][256];                                                    \
+    __shared__ unsigned name##_sel[kBlock / 64][kEstSel];                                                 \
+    const EstLds name{name##_ent[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6], name##_sel[threadIdx.x >> 6], \
                       (unsigned)(cap)}
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -985,8 +986,14 @@ __global__ void __launch_bounds__(kBlock) k_gather_hit(DevScene S, uint64_t seed
 // the estimate's state: the wave takes its 64 requests one after another, each read through the
 // scalar cache (wave-uniform address), and lane j keeps request j's result for one coalesced store.
 // LDS list capacity kGatherEstCap and <= 96 VGPRs: five waves per SIMD
-constexpr int kGatherEstCap = 768;
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) k_gather_est(
+#ifndef FRT_GATHER_CAP
+#define FRT_GATHER_CAP 768
+#endif
+constexpr int kGatherEstCap = FRT_GATHER_CAP;
+#ifndef FRT_EST_WAVES
+#define FRT_EST_WAVES 4
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8))) k_gather_est(
     DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col) {
     FRT_EST_LDS(lds, kGatherEstCap);
     const int lane = est_lane();
@@ -1028,7 +1035,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 
 
 // frt_pm_estimate's kernel: one wave per query (pos[3], normal[3]), the estimate as lighting_gi
 // calls it before its scaling
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) k_pm_estimate(
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8))) k_pm_estimate(
     PhotonMapDev M, const double* __restrict__ q, int64_t nq, double radius, int k, double cone_k,
     double* __restrict__ irrad, int64_t* __restrict__ found) {
     FRT_EST_LDS(lds, kGatherEstCap);
@@ -2194,9 +2201,9 @@ constexpr double kMaxGridCells = (double)(1 << 24);
 // pm_photon_dir directions): balanced as pm_balance would (heap index per photon, split planes), the
 // photons the reference's search reaches binned into the dense grid (frt_gi.hpp wave_scan_cells; cell
 // edge radius / 3, doubled while the grid would exceed kMaxGridCells; sorted by cell, x fastest, so a
-// row of cells is one contiguous range). One allocation per map: binary32 positions with the heap
-// index in .w | power + direction records | cell starts | the kd-tree (binary64 position and split
-// plane per heap index: the exact distances and the traversal order of the estimate).
+// row of cells is one contiguous range). One allocation per map: binary32 positions | 80-byte records
+// (binary64 position, power, direction, heap index) | cell starts | the kd-tree (binary64 position and
+// split plane per heap index: the traversal order of the estimate's selection).
 static int make_photon_map(int64_t n, const double* pos, const double* power, const double* dir,
                            double irradiance_radius, void** out_mem, frt::PhotonMapDev& M) {
     *out_mem = nullptr;
@@ -2257,7 +2264,7 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
     const size_t np = (size_t)std::max<int64_t>(nr, 1);
     std::vector<float> pos4(np * 4, 0.0f);
-    std::vector<double> pwdir(np * 6, 0.0), kd((size_t)(n + 1) * 4, 0.0);
+    std::vector<double> rec(np * 10, 0.0), kd((size_t)(n + 1) * 4, 0.0);
     for (int64_t i = 0; i < n; ++i) {
         const int32_t hx = heap_of[(size_t)i];
         for (int k = 0; k < 3; ++k) kd[(size_t)(4 * hx + k)] = pos[3 * i + k];
@@ -2266,23 +2273,24 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
         const int64_t j = fill[(size_t)cell_of[(size_t)i]]++;
         for (int k = 0; k < 3; ++k) {
             pos4[(size_t)(4 * j + k)] = (float)pos[3 * i + k];
-            pwdir[(size_t)(6 * j + k)] = power[3 * i + k];
-            pwdir[(size_t)(6 * j + 3 + k)] = dir[3 * i + k];
+            rec[(size_t)(10 * j + k)] = pos[3 * i + k];
+            rec[(size_t)(10 * j + 3 + k)] = power[3 * i + k];
+            rec[(size_t)(10 * j + 6 + k)] = dir[3 * i + k];
         }
-        int32_t hb = hx;
-        std::memcpy(&pos4[(size_t)(4 * j + 3)], &hb, sizeof(hb));
+        const int64_t hb = hx;
+        std::memcpy(&rec[(size_t)(10 * j + 9)], &hb, sizeof(hb));
     }
-    const size_t b_pos4 = pos4.size() * sizeof(float), b_pw = pwdir.size() * sizeof(double);
+    const size_t b_pos4 = pos4.size() * sizeof(float), b_pw = rec.size() * sizeof(double);
     const size_t b_start = start.size() * sizeof(int32_t), b_kd = kd.size() * sizeof(double);
     const size_t o_kd = (b_pos4 + b_pw + b_start + 63) & ~(size_t)63;
     FRT_HIP(hipMalloc(out_mem, o_kd + b_kd));
     char* mem = (char*)*out_mem;
     FRT_HIP(hipMemcpy(mem, pos4.data(), b_pos4, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4, pwdir.data(), b_pw, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4, rec.data(), b_pw, hipMemcpyHostToDevice));
     FRT_HIP(hipMemcpy(mem + b_pos4 + b_pw, start.data(), b_start, hipMemcpyHostToDevice));
     FRT_HIP(hipMemcpy(mem + o_kd, kd.data(), b_kd, hipMemcpyHostToDevice));
     M.pos4 = (const float*)mem;
-    M.pwdir = (const double*)(mem + b_pos4);
+    M.rec = (const double*)(mem + b_pos4);
     M.start = (const int32_t*)(mem + b_pos4 + b_pw);
     M.kd = (const double*)(mem + o_kd);
     return 0;
@@ -2424,10 +2432,10 @@ static void dump_walk_stats(frt_scene_handle* h) {
     const char* pn[8] = {"setup", "close", "xf_pop", "composite", "leaf_xf", "leaf_test", "leaf_post", "loop"};
     for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s=%llu", pn[k], c[frt::kDbgProf + k]);
     std::fprintf(stderr, "\nestimate prof (cycles): scan=%llu select=%llu sum=%llu band=%llu; queries over k=%llu "
-                 "unlisted=%llu slow_band=%llu order_check=%llu in_range_total=%llu",
+                 "unlisted=%llu slow_band=%llu order_check=%llu in_range_total=%llu order_check_cycles=%llu",
                  c[frt::kDbgProf + 13], c[frt::kDbgProf + 14], c[frt::kDbgProf + 15], c[frt::kDbgProf + 16],
                  c[frt::kDbgProf + 17], c[frt::kDbgProf + 18], c[frt::kDbgProf + 19], c[frt::kDbgProf + 20],
-                 c[frt::kDbgProf + 21]);
+                 c[frt::kDbgProf + 21], c[frt::kDbgProf + 22]);
     std::fprintf(stderr, "\nprepare prof (cycles):");
     const char* qn[5] = {"ray", "hits_load", "prepare", "spawn", "stores"};
     for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s=%llu", qn[k], c[frt::kDbgProf + 8 + k]);

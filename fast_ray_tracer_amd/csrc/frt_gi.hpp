@@ -84,9 +84,12 @@ __device__ inline void hemisphere_dir(const double* n, const double* nt, const d
 // is not stored: the passes then re-scan the rows.
 constexpr int kEstCap = 1024;
 
+constexpr unsigned kEstSel = 256;
+
 struct EstLds {
     uint2* ent;       // cap: (squared distance bits, photon index) of the photons within the radius
     unsigned* hist;   // 256
+    unsigned* sel;    // kEstSel: the photons the sum pass certainly takes (their records load together)
     unsigned cap;
 };
 
@@ -137,7 +140,7 @@ __device__ __forceinline__ unsigned est_key(float d2, float inv_r2) {
 // within the radius. The visiting order (rows in (z, y) order, photons in grid
 // order) is the same in every pass.
 template <typename F>
-__device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, double r, float r2f, F&& f) {
+__device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const double* x, double r, float r2f, F&& f) {
     const int lane = est_lane();
     const double ax = fmax(fmax(fabs(x[0]), fabs(x[1])), fabs(x[2]));
     const double re = r * (1.0 + 1e-5) + 0x1p-20 * ax;
@@ -199,57 +202,95 @@ __device__ inline void wave_scan_cells(const PhotonMapDev& M, const double* x, d
             }
             return o + (int32_t)g;
         };
-        // two chunks per step: both position loads are in flight before either is used
-        for (unsigned base = 0; base < total; base += 128) {
-            const int32_t pa = chunk_photon(base), pb = chunk_photon(base + 64u);
-            bool ina = base + (unsigned)lane < total, inb = base + 64u + (unsigned)lane < total;
-            float4 qa = make_float4(0.0f, 0.0f, 0.0f, 0.0f), qb = qa;
-            if (ina) qa = reinterpret_cast<const float4*>(M.pos4)[pa];
-            if (inb) qb = reinterpret_cast<const float4*>(M.pos4)[pb];
-            float d2a = 0.0f, d2b = 0.0f;
-            if (ina) {
-                const float dx = qa.x - xf[0], dy = qa.y - xf[1], dz = qa.z - xf[2];
-                d2a = dx * dx + dy * dy + dz * dz;
-                ina = d2a < r2f;
+        // kScanChunks chunks per step: their position loads are all in flight before any is used
+#ifndef FRT_SCAN_CHUNKS
+#define FRT_SCAN_CHUNKS 2
+#endif
+        constexpr int kScanChunks = FRT_SCAN_CHUNKS;
+        for (unsigned base = 0; base < total; base += 64u * kScanChunks) {
+            int32_t pc[kScanChunks];
+            bool inc[kScanChunks];
+            float4 qc[kScanChunks];
+#pragma unroll
+            for (int c = 0; c < kScanChunks; ++c) {
+                pc[c] = chunk_photon(base + 64u * c);
+                inc[c] = base + 64u * c + (unsigned)lane < total;
+                qc[c] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (inc[c]) qc[c] = reinterpret_cast<const float4*>(M.pos4)[pc[c]];
             }
-            if (inb) {
-                const float dx = qb.x - xf[0], dy = qb.y - xf[1], dz = qb.z - xf[2];
-                d2b = dx * dx + dy * dy + dz * dz;
-                inb = d2b < r2f;
+#pragma unroll
+            for (int c = 0; c < kScanChunks; ++c) {
+                if (base + 64u * c >= total) break;  // (uniform)
+                float d2 = 0.0f;
+                bool in = inc[c];
+                if (in) {
+                    const float dx = qc[c].x - xf[0], dy = qc[c].y - xf[1], dz = qc[c].z - xf[2];
+                    d2 = dx * dx + dy * dy + dz * dz;
+                    in = d2 < r2f;
+                }
+                f(pc[c], in, d2);
             }
-            f(pa, ina, d2a);
-            f(pb, inb, d2b);
         }
     }
 }
 
-// the binary64 squared distance of heap photon h in the reference's order (pm.c:188-193)
-__device__ __forceinline__ double kd_d2(const double* __restrict__ kd, int32_t h, const double* x) {
-    const double2* q = reinterpret_cast<const double2*>(kd + 4 * (int64_t)h);
-    const double2 a = q[0], b = q[1];
-    double d = a.x - x[0];
-    double d2 = d * d;
-    d = a.y - x[1];
-    d2 += d * d;
-    d = b.x - x[2];
-    d2 += d * d;
-    return d2;
+// one photon's 80-byte record (grid order): binary64 position, power, direction, heap index
+struct PhotonRec {
+    double2 r[5];
+    __device__ __forceinline__ double d2(const double* x) const {  // pm.c:188-193, the reference's order
+        double d = r[0].x - x[0];
+        double v = d * d;
+        d = r[0].y - x[1];
+        v += d * d;
+        d = r[1].x - x[2];
+        v += d * d;
+        return v;
+    }
+    __device__ __forceinline__ int32_t heap() const { return (int32_t)__double_as_longlong(r[4].y); }
+};
+
+__device__ __forceinline__ PhotonRec photon_rec(const PhotonMapDev& M, int32_t p) {
+    const double2* q = reinterpret_cast<const double2*>(M.rec) + 5 * (int64_t)p;
+    PhotonRec o;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) o.r[j] = q[j];
+    return o;
 }
 
-__device__ __forceinline__ int32_t heap_of(const PhotonMapDev& M, int32_t p) {
-    return __float_as_int(M.pos4[4 * (int64_t)p + 3]);
+// the binary64 squared distance alone (the first 32 bytes of the record)
+__device__ __forceinline__ double photon_d2(const PhotonMapDev& M, int32_t p, const double* x) {
+    const double2* q = reinterpret_cast<const double2*>(M.rec) + 5 * (int64_t)p;
+    const double2 a = q[0], b = q[1];
+    double d = a.x - x[0];
+    double v = d * d;
+    d = a.y - x[1];
+    v += d * d;
+    d = b.x - x[2];
+    v += d * d;
+    return v;
+}
+
+__device__ __forceinline__ int32_t photon_heap(const PhotonMapDev& M, int32_t p) {
+    return (int32_t)__double_as_longlong(M.rec[10 * (int64_t)p + 9]);
+}
+
+// the traversal of query x visits heap node c's right child first (pm.c:173-183: dist1 = x[plane] -
+// p[plane] > 0); the node's 32 bytes in one round trip
+__device__ __forceinline__ bool kd_right_first(const double* __restrict__ kd, int32_t c, const double* x) {
+    const double2* q = reinterpret_cast<const double2*>(kd + 4 * (int64_t)c);
+    const double2 a = q[0], b = q[1];
+    const int ax = (int)b.y;
+    const double split = ax == 0 ? a.x : (ax == 1 ? a.y : b.x);
+    const double xa = ax == 0 ? x[0] : (ax == 1 ? x[1] : x[2]);
+    return xa - split > 0.0;
 }
 
 // (all lanes) bit j: at the ancestor of heap node q at depth j (root 0), the query's traversal visits
-// the right child first (pm.c:173-183: dist1 = x[plane] - p[plane] > 0)
+// the right child first
 __device__ __forceinline__ unsigned near_mask(const double* __restrict__ kd, int32_t q, const double* x) {
     const int dq = 31 - __clz(q), lane = est_lane();
     bool right = false;
-    if (lane < dq) {
-        const double* c = kd + 4 * (int64_t)(q >> (dq - lane));
-        const int ax = (int)c[3];
-        right = x[ax] - c[ax] > 0.0;
-    }
+    if (lane < dq) right = kd_right_first(kd, q >> (dq - lane), x);
     return (unsigned)__ballot(right);
 }
 
@@ -272,15 +313,11 @@ __device__ __forceinline__ bool found_before_any(const double* __restrict__ kd, 
     const int m = min(da, db);
     const int32_t a2 = a >> (da - m), b2 = b >> (db - m);
     const int up = 32 - __clz(a2 ^ b2);
-    const double* c = kd + 4 * (int64_t)(a2 >> up);
-    const int ax = (int)c[3];
-    return ((a2 >> (up - 1)) & 1) == (x[ax] - c[ax] > 0.0 ? 1 : 0);
+    return ((a2 >> (up - 1)) & 1) == (kd_right_first(kd, a2 >> up, x) ? 1 : 0);
 }
 
 __device__ __forceinline__ unsigned wave_and(bool v) { return __ballot(!v) == 0ull ? 1u : 0u; }
 
-// all 64 lanes call with the same x / normal; returns the photons used (the reference's `found`) and
-// the irradiance, in every lane
 #ifdef FRT_WALK_PROF
 #define EST_STAMP(k)                                                                      \
     do {                                                                                  \
@@ -296,7 +333,33 @@ __device__ __forceinline__ unsigned wave_and(bool v) { return __ballot(!v) == 0u
 #define EST_STAMP(k)
 #define EST_COUNT(k, v)
 #endif
-__device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
+
+// the digit of rank `need` (1-based) in a 256-bin histogram held 4 bins per lane: its bin, count, and
+// the entries in lower bins (wave-uniform results)
+__device__ __forceinline__ void radix_pick(const unsigned* c4, unsigned need, unsigned& bin, unsigned& cnt,
+                                           unsigned& below) {
+    const int lane = est_lane();
+    unsigned local = c4[0] + c4[1] + c4[2] + c4[3];
+    const unsigned incl = wave_incl_scan(local);
+    const int owner = __builtin_ctzll(__ballot(incl >= need));
+    unsigned b = incl - local, c = c4[3];
+    int bi = 4 * lane + 3;
+    for (int j = 0; j < 4; ++j) {
+        if (b + c4[j] >= need) {
+            bi = 4 * lane + j;
+            c = c4[j];
+            break;
+        }
+        b += c4[j];
+    }
+    bin = (unsigned)__builtin_amdgcn_readlane(bi, owner);
+    cnt = (unsigned)__builtin_amdgcn_readlane((int)c, owner);
+    below = (unsigned)__builtin_amdgcn_readlane((int)b, owner);
+}
+
+// all 64 lanes call with the same x / normal; returns the photons used (the reference's `found`) and
+// the irradiance, in every lane
+__device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
                                                    double max_dist, int k, double cone_k, double* irrad,
                                                    const EstLds& L, unsigned long long* prof = nullptr) {
     irrad[0] = irrad[1] = irrad[2] = 0.0;
@@ -315,14 +378,14 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     const float lo_thr = __double2float_rd(r2 - tol), hi_thr = __double2float_ru(r2 + tol);
     const float inv_r2 = (float)(1.0 / r2);
     // keys closer than dk may belong to photons whose binary64 order differs from their keys' order
-    // (2 tol, the key's own rounding (3u relative) and its truncation)
-    const unsigned dk = (unsigned)ceil((2.0 * tol + 8.0 * 0x1p-24 * r2) * (16777216.0 / r2)) + 3u;
+    // (2 tol, the key's own rounding (3u relative) and its truncation); dk < 2^16 for any sane radius
+    const unsigned dk = min((unsigned)ceil((2.0 * tol + 8.0 * 0x1p-24 * r2) * (16777216.0 / r2)) + 3u, 65535u);
     // within the radius, exactly: binary32 away from it, binary64 near it (uniform control flow)
     auto in_range = [&](int32_t p, bool cand, float d2) {
         bool in = cand && d2 < lo_thr;
         const bool unc = cand && !in;
         if (__ballot(unc)) {
-            if (unc) in = kd_d2(M.kd, heap_of(M, p), x) < r2;
+            if (unc) in = photon_d2(M, p, x) < r2;
         }
         return in;
     };
@@ -345,39 +408,72 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     EST_STAMP(0);
     const unsigned found = total < (unsigned)k ? total : (unsigned)k;
     if (found < 8) return found;
-    const bool listed = total <= L.cap;
+    unsigned h4[4];  // the first digit's histogram
+    for (int j = 0; j < 4; ++j) h4[j] = L.hist[4 * lane + j];
+    // the list: every photon in range or, when they overflow the wave's LDS and the heap decides,
+    // those whose key's top digit is at most one beyond the (k+1)-th's (which covers the band, dk <
+    // 2^16), stored by a second scan; only the rare traversal-order check needs the others (re-scan)
+    unsigned count = total;
+    bool listed = total <= L.cap, filtered = false;
+    if (!listed && total > (unsigned)k) {
+        unsigned b1, c1, below1;
+        radix_pick(h4, (unsigned)k + 1u, b1, c1, below1);
+        const unsigned top = min(b1 + 1u, 255u);
+        unsigned le = 0;
+        for (int j = 0; j < 4; ++j) le += (unsigned)(4 * lane + j) <= top ? h4[j] : 0u;
+        const unsigned n_le = (unsigned)__builtin_amdgcn_readlane((int)wave_incl_scan(le), 63);
+        if (n_le <= L.cap) {
+            unsigned at0 = 0;
+            wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) {
+                const bool keep = in_range(p, cand, d2) && (est_key(d2, inv_r2) >> 16) <= top;
+                const unsigned long long m = __ballot(keep);
+                if (keep) L.ent[at0 + (unsigned)__popcll(m & ((1ull << lane) - 1))] = make_uint2(__float_as_uint(d2), (unsigned)p);
+                at0 += (unsigned)__popcll(m);
+            });
+            __builtin_amdgcn_wave_barrier();
+            count = at0;
+            listed = filtered = true;
+        }
+    }
     EST_COUNT(4, total > (unsigned)k ? 1ull : 0ull);
     EST_COUNT(5, listed ? 0ull : 1ull);
     EST_COUNT(8, (unsigned long long)total);
-    // every pass visits the photons in range in the same order: from the list, or a re-scan
+    // every pass visits the listed photons in the same order (the list, or a re-scan when unlisted);
+    // visit_all also the ones a filtered list omits
+    auto scan_all = [&](auto&& fn) {
+        wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) { fn(p, in_range(p, cand, d2), d2); });
+    };
     auto visit = [&](auto&& fn) {
         if (listed) {
-            for (unsigned base = 0; base < total; base += 64) {
+            for (unsigned base = 0; base < count; base += 64) {
                 const unsigned i = base + (unsigned)lane;
-                const bool in = i < total;
+                const bool in = i < count;
                 const uint2 e = in ? L.ent[i] : make_uint2(0u, 0u);
                 fn((int32_t)e.y, in, __uint_as_float(e.x));
             }
         } else {
-            wave_scan_cells(M, x, max_dist, hi_thr,
-                            [&](int32_t p, bool cand, float d2) { fn(p, in_range(p, cand, d2), d2); });
+            scan_all(fn);
         }
     };
-    // one 48-byte record per photon: power x, y, z, direction x, y, z
-    auto record = [&](int32_t p, double2* r) {
-        const double2* rec = reinterpret_cast<const double2*>(M.pwdir) + 3 * (int64_t)p;
-        r[0] = rec[0];
-        r[1] = rec[1];
-        r[2] = rec[2];
+    auto visit_all = [&](auto&& fn) {
+        if (filtered) scan_all(fn);
+        else visit(fn);
     };
     const double cone_r = cone_k * max_dist;
     double acc[3] = {0.0, 0.0, 0.0};
-    auto accumulate = [&](double dp, const double2* r) {
+    auto photon_weighted = [&](const PhotonRec& pr, double dp, double* w) {  // pm.c:129-145
         const double weight = 1.0 - dp / cone_r;
-        if ((r[1].y * normal[0] + r[2].x * normal[1] + r[2].y * normal[2]) < 0.0) {
-            acc[0] += r[0].x * weight;
-            acc[1] += r[0].y * weight;
-            acc[2] += r[1].x * weight;
+        const bool facing = (pr.r[3].x * normal[0] + pr.r[3].y * normal[1] + pr.r[4].x * normal[2]) < 0.0;
+        w[0] = facing ? pr.r[1].y * weight : 0.0;
+        w[1] = facing ? pr.r[2].x * weight : 0.0;
+        w[2] = facing ? pr.r[2].y * weight : 0.0;
+    };
+    auto accumulate = [&](const PhotonRec& pr, double dp) {
+        const double weight = 1.0 - dp / cone_r;
+        if ((pr.r[3].x * normal[0] + pr.r[3].y * normal[1] + pr.r[4].x * normal[2]) < 0.0) {
+            acc[0] += pr.r[1].y * weight;
+            acc[1] += pr.r[2].x * weight;
+            acc[2] += pr.r[2].y * weight;
         }
     };
     auto finish = [&](double d0) {
@@ -389,94 +485,90 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         irrad[2] *= tmp;
     };
     if (total <= (unsigned)k) {  // every photon in range: no heap, dist2[0] = max_dist^2
-        visit([&](int32_t p, bool in, float d2) {
+        visit([&](int32_t p, bool in, float) {
             if (in) {
-                double2 r[3];
-                record(p, r);
-                accumulate(sqrt(kd_d2(M.kd, heap_of(M, p), x)), r);
+                const PhotonRec pr = photon_rec(M, p);
+                accumulate(pr, sqrt(pr.d2(x)));
             }
         });
         finish(r2);
         EST_STAMP(2);
         return found;
     }
-    // ---- the k-th and (k+1)-th keys: radix selects, 8 bits per digit ----
-    unsigned h4[4];  // the first digit's histogram, kept for the second select
-    for (int j = 0; j < 4; ++j) h4[j] = L.hist[4 * lane + j];
-    auto select = [&](unsigned need, unsigned& lo, unsigned& hi) {
-        unsigned prefix = 0, mask = 0;
-        for (int shift = 16; shift >= 0; shift -= 8) {
-            unsigned c4[4], local = 0;
-            if (shift == 16) {
-                for (int j = 0; j < 4; ++j) c4[j] = h4[j];
-            } else {
+    // ---- the k-th and (k+1)-th keys: radix selects, 8 bits per digit, sharing a histogram pass while
+    // both ranks lie under the same prefix ----
+    unsigned need_s[2] = {(unsigned)k, (unsigned)k + 1u}, prefix[2], mask[2] = {0xFF0000u, 0xFF0000u};
+    bool done[2];
+    for (int s = 0; s < 2; ++s) {
+        unsigned bin, cnt, below;
+        radix_pick(h4, need_s[s], bin, cnt, below);
+        need_s[s] -= below;
+        prefix[s] = bin << 16;
+        done[s] = cnt <= 64u;  // few enough: the band ranks them
+    }
+    for (int shift = 8; shift >= 0 && !(done[0] && done[1]); shift -= 8) {
+        const bool shared = !done[0] && !done[1] && prefix[0] == prefix[1];
+        unsigned c4[4];
+        for (int s = 0; s < 2; ++s) {
+            if (done[s]) continue;
+            if (!(s == 1 && shared)) {
                 for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
                 __builtin_amdgcn_wave_barrier();
+                const unsigned pf = prefix[s], mk = mask[s];
                 visit([&](int32_t, bool in, float d2) {
                     const unsigned key = est_key(d2, inv_r2);
-                    if (in && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
+                    if (in && (key & mk) == pf) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
                 });
                 __builtin_amdgcn_wave_barrier();
                 for (int j = 0; j < 4; ++j) c4[j] = L.hist[4 * lane + j];
             }
-            for (int j = 0; j < 4; ++j) local += c4[j];
-            const unsigned incl = wave_incl_scan(local);
-            const int owner = __builtin_ctzll(__ballot(incl >= need));
-            unsigned below = incl - local, cnt = c4[3];
-            int bin = 4 * lane + 3;
-            for (int j = 0; j < 4; ++j) {
-                if (below + c4[j] >= need) {
-                    bin = 4 * lane + j;
-                    cnt = c4[j];
-                    break;
-                }
-                below += c4[j];
-            }
-            bin = __builtin_amdgcn_readlane(bin, owner);
-            cnt = __builtin_amdgcn_readlane(cnt, owner);
-            below = __builtin_amdgcn_readlane(below, owner);
-            need -= below;
-            prefix |= (unsigned)bin << shift;
-            mask |= 255u << shift;
-            if (cnt <= 64u) break;  // few enough: the band ranks them
+            unsigned bin, cnt, below;
+            radix_pick(c4, need_s[s], bin, cnt, below);
+            need_s[s] -= below;
+            prefix[s] |= bin << shift;
+            mask[s] |= 255u << shift;
+            done[s] = cnt <= 64u || shift == 0;
         }
-        lo = prefix;
-        hi = prefix | (~mask & 0xFFFFFFu);
-    };
-    unsigned klo, khi, k1lo, k1hi;
-    select((unsigned)k, klo, khi);
-    select((unsigned)k + 1u, k1lo, k1hi);
+    }
+    const unsigned klo = prefix[0], k1hi = prefix[1] | (~mask[1] & 0xFFFFFFu);
     const unsigned blo = klo > dk ? klo - dk : 0u, bhi = min(k1hi + dk, 0xFFFFFFu);
     EST_STAMP(1);
     // ---- the band: ranked by binary64 distance ----
     // pass B: photons with keys in [blo, bhi] set aside (up to 64, in L.hist), the certain ones counted
+    // and the certain ones' indices compacted into L.sel (while they fit)
     unsigned c_in = 0, nb = 0;
     visit([&](int32_t p, bool in, float d2) {
         const unsigned key = est_key(d2, inv_r2);
-        const bool band = in && key >= blo && key <= bhi;
-        const unsigned long long bm = __ballot(band);
+        const bool band = in && key >= blo && key <= bhi, cert = in && key < blo;
+        const unsigned long long lt = (1ull << lane) - 1;
+        const unsigned long long bm = __ballot(band), cm = __ballot(cert);
         if (band) {
-            const unsigned at = nb + (unsigned)__popcll(bm & ((1ull << lane) - 1));
+            const unsigned at = nb + (unsigned)__popcll(bm & lt);
             if (at < 64u) L.hist[at] = (unsigned)p;
         }
+        if (cert) {
+            const unsigned at = c_in + (unsigned)__popcll(cm & lt);
+            if (at < kEstSel) L.sel[at] = (unsigned)p;
+        }
         nb += (unsigned)__popcll(bm);
-        c_in += (unsigned)__popcll(__ballot(in && key < blo));
+        c_in += (unsigned)__popcll(cm);
     });
     __builtin_amdgcn_wave_barrier();
     const unsigned need = (unsigned)k - c_in;  // band ranks of the k-th (need - 1) and the (k+1)-th (need)
     double vk = r2, vk1 = r2;
     int32_t R = 1;
     bool mine_band = false;  // this lane holds a band photon (fast path)
-    int32_t bp = 0, bh = 1;
-    double bv = 0.0;
+    int32_t bh = 1;
+    double bv = 0.0, bw[3] = {0.0, 0.0, 0.0};  // its binary64 distance, weighted power (0: facing away)
     unsigned brank = 0;
     const bool fast = nb <= 64u && need >= 1u && need + 1u <= nb;
     if (fast) {
         mine_band = (unsigned)lane < nb;
         if (mine_band) {
-            bp = (int32_t)L.hist[lane];
-            bh = heap_of(M, bp);
-            bv = kd_d2(M.kd, bh, x);
+            const PhotonRec pr = photon_rec(M, (int32_t)L.hist[lane]);
+            bv = pr.d2(x);
+            bh = pr.heap();
+            photon_weighted(pr, sqrt(bv), bw);
         }
         for (unsigned j = 0; j < nb; ++j) {
             const double vj = readlane_dd(bv, (int)j);
@@ -492,7 +584,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         // many photons in the band (a dense caustic): exact radix selects over the band's binary64
         // distances (their bit patterns order like the values), passes over the list
         auto exact_rank = [&](unsigned rk) {
-            unsigned long long prefix = 0, mask = 0;
+            unsigned long long pf = 0, mk = 0;
             for (int shift = 56; shift >= 0; shift -= 8) {
                 for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
                 __builtin_amdgcn_wave_barrier();
@@ -500,34 +592,19 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
                     const unsigned key = est_key(d2, inv_r2);
                     const bool band = in && key >= blo && key <= bhi;
                     if (band) {
-                        const unsigned long long b = (unsigned long long)__double_as_longlong(kd_d2(M.kd, heap_of(M, p), x));
-                        if ((b & mask) == prefix) atomicAdd(&L.hist[(unsigned)((b >> shift) & 255ull)], 1u);
+                        const unsigned long long b = (unsigned long long)__double_as_longlong(photon_d2(M, p, x));
+                        if ((b & mk) == pf) atomicAdd(&L.hist[(unsigned)((b >> shift) & 255ull)], 1u);
                     }
                 });
                 __builtin_amdgcn_wave_barrier();
-                unsigned c4[4], local = 0;
-                for (int j = 0; j < 4; ++j) {
-                    c4[j] = L.hist[4 * lane + j];
-                    local += c4[j];
-                }
-                const unsigned incl = wave_incl_scan(local);
-                const int owner = __builtin_ctzll(__ballot(incl >= rk));
-                unsigned below = incl - local;
-                int bin = 4 * lane + 3;
-                for (int j = 0; j < 4; ++j) {
-                    if (below + c4[j] >= rk) {
-                        bin = 4 * lane + j;
-                        break;
-                    }
-                    below += c4[j];
-                }
-                bin = __builtin_amdgcn_readlane(bin, owner);
-                below = __builtin_amdgcn_readlane(below, owner);
+                unsigned c4[4], bin, cnt, below;
+                for (int j = 0; j < 4; ++j) c4[j] = L.hist[4 * lane + j];
+                radix_pick(c4, rk, bin, cnt, below);
                 rk -= below;
-                prefix |= (unsigned long long)bin << shift;
-                mask |= 255ull << shift;
+                pf |= (unsigned long long)bin << shift;
+                mk |= 255ull << shift;
             }
-            return __longlong_as_double((long long)prefix);
+            return __longlong_as_double((long long)pf);
         };
         vk = exact_rank(need);
         vk1 = exact_rank(need + 1u);
@@ -535,10 +612,7 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         visit([&](int32_t p, bool in, float d2) {  // the (k+1)-th's heap index (first of equal distances)
             const unsigned key = est_key(d2, inv_r2);
             int32_t hx = 0;
-            if (in && key >= blo && key <= bhi) {
-                hx = heap_of(M, p);
-                if (kd_d2(M.kd, hx, x) != vk1) hx = 0;
-            }
+            if (in && key >= blo && key <= bhi && photon_d2(M, p, x) == vk1) hx = photon_heap(M, p);
             const unsigned long long hm = __ballot(hx != 0);
             if (rh == 0 && hm) rh = __builtin_amdgcn_readlane(hx, __builtin_ctzll(hm));
         });
@@ -546,39 +620,54 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
     }
     EST_STAMP(3);
     // ---- sum pass over the k nearest, checking that each comes before the (k+1)-th ----
-    const unsigned qmask = near_mask(M.kd, R, x);
     bool before_all = true;
     unsigned below_k = 0;  // (slow path) band photons strictly nearer than the k-th
-    auto band_member = [&](double v) { return v <= vk; };
-    visit([&](int32_t p, bool in, float d2) {
+    const bool compact = c_in <= kEstSel;
+    // the certain photons from L.sel, two chunks' records in flight together; the first two chunks'
+    // loads issue with near_mask's
+    const unsigned qmask = near_mask(M.kd, R, x);
+    if (compact) {
+        for (unsigned base = 0; base < c_in; base += 128) {
+            const unsigned i0 = base + (unsigned)lane, i1 = i0 + 64u;
+            const bool a = i0 < c_in, b = i1 < c_in;
+            PhotonRec ra, rb;
+            if (a) ra = photon_rec(M, (int32_t)L.sel[i0]);
+            if (b) rb = photon_rec(M, (int32_t)L.sel[i1]);
+            if (a) {
+                accumulate(ra, sqrt(ra.d2(x)));
+                before_all = before_all && found_before(ra.heap(), R, qmask);
+            }
+            if (b) {
+                accumulate(rb, sqrt(rb.d2(x)));
+                before_all = before_all && found_before(rb.heap(), R, qmask);
+            }
+        }
+    }
+    if (!compact || !fast) visit([&](int32_t p, bool in, float d2) {
         const unsigned key = est_key(d2, inv_r2);
-        const bool certain = in && key < blo;
+        const bool certain = in && key < blo && !compact;
         const bool band = in && key >= blo && key <= bhi && !fast;
         if (certain) {
-            const int32_t hx = heap_of(M, p);
-            double2 r[3];
-            record(p, r);
-            accumulate(sqrt(kd_d2(M.kd, hx, x)), r);
-            before_all = before_all && found_before(hx, R, qmask);
+            const PhotonRec pr = photon_rec(M, p);
+            accumulate(pr, sqrt(pr.d2(x)));
+            before_all = before_all && found_before(pr.heap(), R, qmask);
         }
         if (__ballot(band)) {  // (slow path) band photons: membership by their binary64 distance
             bool nearer = false;
             if (band) {
-                const int32_t hx = heap_of(M, p);
-                const double v = kd_d2(M.kd, hx, x);
+                const PhotonRec pr = photon_rec(M, p);
+                const double v = pr.d2(x);
                 nearer = v < vk;
-                if (nearer) {  // those at the k-th's and the (k+1)-th's distance are added after the check
-                    double2 r[3];
-                    record(p, r);
-                    accumulate(sqrt(v), r);
-                }
-                if (band_member(v) && hx != R) before_all = before_all && found_before(hx, R, qmask);
+                // those at the k-th's and the (k+1)-th's distance are added after the check
+                if (nearer) accumulate(pr, sqrt(v));
+                if (v <= vk && pr.heap() != R) before_all = before_all && found_before(pr.heap(), R, qmask);
             }
             below_k += (unsigned)__popcll(__ballot(nearer));
         }
     });
     if (fast && mine_band && brank < need) before_all = before_all && found_before(bh, R, qmask);
     bool quirk = false;
+    EST_STAMP(2);
     if (wave_and(before_all)) {
         // every one of the k nearest precedes the (k+1)-th: the traversal may have found them first.
         // The last of them in traversal order, then every other photon in range against it.
@@ -589,11 +678,8 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         };
         visit([&](int32_t p, bool in, float d2) {
             const unsigned key = est_key(d2, inv_r2);
-            if (in && key < blo) consider(heap_of(M, p));
-            if (in && key >= blo && key <= bhi && !fast) {
-                const int32_t hx = heap_of(M, p);
-                if (band_member(kd_d2(M.kd, hx, x))) consider(hx);
-            }
+            if (in && key < blo) consider(photon_heap(M, p));
+            if (in && key >= blo && key <= bhi && !fast && photon_d2(M, p, x) <= vk) consider(photon_heap(M, p));
         });
         if (fast && mine_band && brank < need) consider(bh);
 #pragma unroll
@@ -604,27 +690,21 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
         const int32_t Lh = __builtin_amdgcn_readlane(last, 0);
         const unsigned lmask = near_mask(M.kd, Lh, x);
         bool after = true;
-        visit([&](int32_t p, bool in, float d2) {
+        visit_all([&](int32_t p, bool in, float d2) {
             const unsigned key = est_key(d2, inv_r2);
             bool other = in && key > bhi;
-            int32_t hx = 0;
-            if (in && key >= blo && key <= bhi && !fast) {
-                hx = heap_of(M, p);
-                other = !band_member(kd_d2(M.kd, hx, x));
-            }
-            if (other) after = after && !found_before(hx != 0 ? hx : heap_of(M, p), Lh, lmask);
+            if (in && key >= blo && key <= bhi && !fast) other = photon_d2(M, p, x) > vk;
+            if (other) after = after && !found_before(photon_heap(M, p), Lh, lmask);
         });
         if (fast && mine_band && brank >= need) after = after && !found_before(bh, Lh, lmask);
         quirk = wave_and(after);
+        EST_STAMP(9);
     }
     // the band's selected photons: ranks below need (the k-th excluded and the (k+1)-th included when
     // the traversal found the k nearest first)
     if (fast) {
-        if (mine_band && (quirk ? (brank + 1u < need || brank == need) : brank < need)) {
-            double2 r[3];
-            record(bp, r);
-            accumulate(sqrt(bv), r);
-        }
+        if (mine_band && (quirk ? (brank + 1u < need || brank == need) : brank < need))
+            for (int j = 0; j < 3; ++j) acc[j] += bw[j];
     } else {
         // slow path: photons at the k-th's distance up to rank k (rank k - 1 when the (k+1)-th replaces
         // the k-th), then the (k+1)-th (ties: the first ones visited)
@@ -638,15 +718,12 @@ __device__ inline int64_t wave_irradiance_estimate(const PhotonMapDev& M, const 
             const bool band = in && key >= blo && key <= bhi;
             if (__ballot(band)) {
                 double v = -1.0;
-                if (band) v = kd_d2(M.kd, heap_of(M, p), x);
+                if (band) v = photon_d2(M, p, x);
                 const bool ek = band && v == vk, ek1 = band && v == vk1 && vk1 != vk;
                 const unsigned long long below = (1ull << lane) - 1;
                 const unsigned long long mk = __ballot(ek), mk1 = __ballot(ek1);
-                if ((ek && (unsigned)__popcll(mk & below) < take_k) || (ek1 && (unsigned)__popcll(mk1 & below) < take_k1)) {
-                    double2 r[3];
-                    record(p, r);
-                    accumulate(sqrt(v), r);
-                }
+                if ((ek && (unsigned)__popcll(mk & below) < take_k) || (ek1 && (unsigned)__popcll(mk1 & below) < take_k1))
+                    accumulate(photon_rec(M, p), sqrt(v));
                 take_k -= min(take_k, (unsigned)__popcll(mk));
                 take_k1 -= min(take_k1, (unsigned)__popcll(mk1));
             }

@@ -94,12 +94,13 @@ __device__ __forceinline__ void frame_cache(const Ray& r, FrameCache& c) {
 // (x fastest, so a row of cells is one contiguous photon range), built on the
 // host after tracing
 struct PhotonMapDev {
-    const float* pos4;    // 4 per photon: binary32 x, y, z, heap index (int bits) (the estimate's candidate scan)
-    const double* pwdir;  // 6 per photon: power (scaled by 1 / photon_count), then pm_photon_dir of
-                          // the stored theta / phi bytes (pm.c:80-88)
+    const float* pos4;    // 4 per photon: binary32 x, y, z, 0 (the estimate's candidate scan)
+    const double* rec;    // 10 per photon (80 bytes, grid order like pos4): binary64 x, y, z, power (scaled by
+                          // 1 / photon_count), pm_photon_dir of the stored theta / phi bytes (pm.c:80-88),
+                          // the heap index (int64 bits)
     const int32_t* start; // cell -> first photon, cells + 1 entries
     const double* kd;     // 4 per heap index (pm_balance's kd-tree, frt_engine.hip pm_balance_heap): binary64
-                          // x, y, z and the split plane; .w of pos4 holds each photon's heap index
+                          // x, y, z and the split plane (the traversal order of the estimate's selection)
     int64_t count;        // photons in the grid (those the reference's search reaches)
     int32_t dims[3];      // cells per axis
     int32_t pad;
