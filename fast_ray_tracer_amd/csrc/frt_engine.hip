@@ -810,12 +810,13 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
 }
 
 // the wave's LDS for wave_irradiance_estimate (frt_gi.hpp); blocks of kBlock threads
-#define FRT_EST_LDS(name, cap)                                                                            \
-    __shared__ uint2 name##_ent[kBlock / 64][cap];                                                        \
-    __shared__ unsigned name##_hist[kBlock / 64][256];                                                    \
-    __shared__ unsigned name##_sel[kBlock / 64][kEstSel];                                                 \
+#define FRT_EST_LDS_W(name, cap, waves)                                                                   \
+    __shared__ uint2 name##_ent[waves][cap];                                                              \
+    __shared__ unsigned name##_hist[waves][256];                                                          \
+    __shared__ unsigned name##_sel[waves][kEstSel];                                                       \
     const EstLds name{name##_ent[threadIdx.x >> 6], name##_hist[threadIdx.x >> 6], name##_sel[threadIdx.x >> 6], \
                       (unsigned)(cap)}
+#define FRT_EST_LDS(name, cap) FRT_EST_LDS_W(name, cap, kBlock / 64)
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -983,9 +984,12 @@ __global__ void __launch_bounds__(kBlock) k_gather_hit(DevScene S, uint64_t seed
 }
 
 // the gather hits' photon estimates (lighting_gi, renderer.c:863-892) in a kernel that holds only
-// the estimate's state: the wave takes its 64 requests one after another, each read through the
-// scalar cache (wave-uniform address), and lane j keeps request j's result for one coalesced store.
-// LDS list capacity kGatherEstCap and <= 96 VGPRs: five waves per SIMD
+// the estimate's state: kGatherReqPerWave consecutive requests per wave, one after another, each read
+// through the scalar cache (wave-uniform address) and estimated by the whole wave; lane 0 stores the
+// result. Measured on cornell_gi_480x270_8x8 (tools/ab_gi.sh): 8 or 64 requests per wave with 1 or 4
+// waves per block land within 3 %; one request per wave (no scratch at all) is 20-70 % slower (a wave
+// launch and LDS setup per request); 3 waves per SIMD (no spills) is 8 % slower than 4 (a few spilled
+// VGPRs).
 #ifndef FRT_GATHER_CAP
 #define FRT_GATHER_CAP 768
 #endif
@@ -993,44 +997,50 @@ constexpr int kGatherEstCap = FRT_GATHER_CAP;
 #ifndef FRT_EST_WAVES
 #define FRT_EST_WAVES 4
 #endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8))) k_gather_est(
-    DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col) {
-    FRT_EST_LDS(lds, kGatherEstCap);
-    const int lane = est_lane();
-    const int64_t base = (int64_t)blockIdx.x * blockDim.x + 64 * __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const double scale_num = 10.0 * (double)S.cfg.irradiance_num;
-    double mine[3] = {0.0, 0.0, 0.0};
-    for (int j = 0; j < 64 && base + j < n; ++j) {
-        const GatherReq& r = req[base + j];
-        if (!r.want) continue;
-        double x[3], nrm[3], e[3], est[3] = {0.0, 0.0, 0.0};
-        for (int k = 0; k < 3; ++k) {
-            x[k] = r.pt[k];
-            nrm[k] = r.ev[k];  // the reference passes eyev as the estimate's normal (renderer.c:875)
-        }
-        const int64_t used = wave_irradiance_estimate(S.pmaps[1], x, nrm, S.cfg.irradiance_radius, S.cfg.irradiance_num,
-                                                      S.cfg.cone_filter_k, e, lds,
-                                                      S.dbg ? S.dbg + kDbgProf + 13 : nullptr);
-        if (used > 0) {
-            const double f = scale_num / (double)used;
-            for (int k = 0; k < 3; ++k) est[k] = e[k] * f;
-        }
-        double out3[3];
-        if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
-            for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
-        } else {
+#ifndef FRT_GATHER_WAVES_PER_BLOCK
+#define FRT_GATHER_WAVES_PER_BLOCK 4
+#endif
+constexpr int kGatherWavesPerBlock = FRT_GATHER_WAVES_PER_BLOCK;
+#ifndef FRT_GATHER_REQ_PER_WAVE
+#define FRT_GATHER_REQ_PER_WAVE 64
+#endif
+constexpr int kGatherReqPerWave = FRT_GATHER_REQ_PER_WAVE;
+__global__ void __launch_bounds__(64 * kGatherWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8)))
+k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col) {
+    FRT_EST_LDS_W(lds, kGatherEstCap, kGatherWavesPerBlock);
+    const int64_t w = (int64_t)blockIdx.x * kGatherWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t t0 = w * kGatherReqPerWave;
+    for (int j = 0; j < kGatherReqPerWave; ++j) {
+        const int64_t t = t0 + j;
+        if (t >= n) break;
+        const GatherReq& r = req[t];
+        double out3[3] = {0.0, 0.0, 0.0};
+        if (r.want) {
+            double x[3], nrm[3], e[3], est[3] = {0.0, 0.0, 0.0};
             for (int k = 0; k < 3; ++k) {
-                double dk = r.kd[k] * est[k];
-                dk = dk * r.edn;
-                out3[k] = dk * kPi;  // shade_hit_gi: x pi
+                x[k] = r.pt[k];
+                nrm[k] = r.ev[k];  // the reference passes eyev as the estimate's normal (renderer.c:875)
+            }
+            const int64_t used = wave_irradiance_estimate(S.pmaps[1], x, nrm, S.cfg.irradiance_radius,
+                                                          S.cfg.irradiance_num, S.cfg.cone_filter_k, e, lds,
+                                                          S.dbg ? S.dbg + kDbgProf + 13 : nullptr);
+            if (used > 0) {
+                const double f = 10.0 * (double)S.cfg.irradiance_num / (double)used;
+                for (int k = 0; k < 3; ++k) est[k] = e[k] * f;
+            }
+            if (S.cfg.visualize_photon_map) {  // lighting_gi returns the raw estimate here too
+                for (int k = 0; k < 3; ++k) out3[k] = est[k] * kPi;  // shade_hit_gi: x pi
+            } else {
+                for (int k = 0; k < 3; ++k) {
+                    double dk = r.kd[k] * est[k];
+                    dk = dk * r.edn;
+                    out3[k] = dk * kPi;  // shade_hit_gi: x pi
+                }
             }
         }
-        if (lane == j)
-            for (int k = 0; k < 3; ++k) mine[k] = out3[k] * r.jit0;
+        if (est_lane() == 0)
+            for (int k = 0; k < 3; ++k) gather_col[3 * t + k] = out3[k] * r.jit0;
     }
-    const int64_t t = base + lane;
-    if (t < n)
-        for (int k = 0; k < 3; ++k) gather_col[3 * t + k] = mine[k];
 }
 
 // frt_pm_estimate's kernel: one wave per query (pos[3], normal[3]), the estimate as lighting_gi
@@ -2390,8 +2400,9 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
             }
             {
                 KTimer te(h, st, 10);
-                hipLaunchKernelGGL(k_gather_est, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, G.greq, rays,
-                                   G.gcol);
+                const int64_t gwaves = (rays + kGatherReqPerWave - 1) / kGatherReqPerWave;
+                hipLaunchKernelGGL(k_gather_est, dim3((unsigned)((gwaves + kGatherWavesPerBlock - 1) / kGatherWavesPerBlock)),
+                                   dim3(64 * kGatherWavesPerBlock), 0, h->stream, h->S, G.greq, rays, G.gcol);
             }
             hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
                                G.fgather);
