@@ -2239,7 +2239,12 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
         first = false;
     }
     M.count = nr;
-    double cell = (irradiance_radius > 0 ? irradiance_radius : 1.0) / 3.0;
+    static const double cell_div = [] {  // FRT_PM_CELL_DIV: cells per radius (A/B experiments only)
+        const char* e = std::getenv("FRT_PM_CELL_DIV");
+        const double v = e ? std::atof(e) : 3.0;
+        return v >= 1.0 && v <= 16.0 ? v : 3.0;
+    }();
+    double cell = (irradiance_radius > 0 ? irradiance_radius : 1.0) / cell_div;
     int64_t dims[3];
     for (;;) {
         double cells = 1.0;
