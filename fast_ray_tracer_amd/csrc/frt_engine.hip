@@ -1873,7 +1873,8 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         const int64_t nblocks = (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
         uint32_t segcap = h->jit_beam_on ? (uint32_t)(((nblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock)
                                          : (uint32_t)std::max<int64_t>(1, npairs);
-        if (grow(&h->mixed, h->mixed_cap, (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
+        // pairs, then their resume values (frt_jit_rt.hpp mix_append)
+        if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
             (void)hipGetLastError();
             h->jit_shadow = nullptr;
             launch_shadow(h, B, rec, n, counts);

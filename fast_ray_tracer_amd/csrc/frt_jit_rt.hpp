@@ -268,7 +268,8 @@ __device__ __forceinline__ void ray64_once(const Lane32& L, bool& have, Ray& r, 
 constexpr int kMixSegs = 64;
 constexpr int kMixLine = 64;  // 32-bit words per counter line
 
-__device__ __forceinline__ void mix_append(bool mix, uint32_t pair, uint32_t* __restrict__ mixed,
+// (the list's second half, at kMixSegs * segcap, holds each pair's resume value at the same slot)
+__device__ __forceinline__ void mix_append(bool mix, uint32_t pair, uint32_t value, uint32_t* __restrict__ mixed,
                                            unsigned* __restrict__ mcount, uint32_t segcap, unsigned* __restrict__ err) {
     const unsigned long long mm = __ballot(mix);
     if (mm == 0) return;
@@ -279,8 +280,12 @@ __device__ __forceinline__ void mix_append(bool mix, uint32_t pair, uint32_t* __
     base = __shfl(base, 0, 64);
     if (mix) {
         const unsigned at = base + (unsigned)__popcll(mm & ((1ull << lane) - 1));
-        if (at < segcap) mixed[(size_t)seg * segcap + at] = pair;
-        else atomicOr(err, kErrQueueOverflow);
+        if (at < segcap) {
+            mixed[(size_t)seg * segcap + at] = pair;
+            mixed[(size_t)kMixSegs * segcap + (size_t)seg * segcap + at] = value;
+        } else {
+            atomicOr(err, kErrQueueOverflow);
+        }
     }
 }
 
