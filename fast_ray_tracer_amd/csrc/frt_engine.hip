@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<Node
 }
 
 // bottom-up combine of one level (shade_hit's specular block, renderer.c:773-822)
-// (level 0: samples land in sample_out at (sub-sample, pixel) order, coalesced for k_resolve)
+// (level 0: samples land in sample_out in sample order, coalesced stores; k_resolve reads each pixel's run)
 __global__ void __launch_bounds__(kBlock) k_combine(Cols<NodeRec> rec, int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
                                                     Cols<Tri9> parent_child, Cols<Tri9> sample_out, int32_t spp,
                                                     const frt_material* __restrict__ mats, int32_t include_specular) {
@@ -588,32 +588,58 @@ __global__ void __launch_bounds__(kBlock) k_combine(Cols<NodeRec> rec, int64_t n
     if (nr.parent >= 0) {
         tri_store(parent_child, 2 * (int64_t)nr.parent + nr.slot, col);  // a missed child writes its zeros
     } else {
-        tri_store(sample_out, (i % spp) * (n / spp) + i / spp, col);
+        tri_store(sample_out, i, col);  // sample order (pixel-major): one coalesced run per column
     }
 }
 
 // pixel_multi_sample + render_multi_helper's (A+D+S)/3 (renderer.c:132-181, 216-233)
-__global__ void __launch_bounds__(kBlock) k_resolve(Cols<Tri9> sample_col, int64_t npix, int32_t spp,
-                                                    double* __restrict__ out) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= npix) return;
-    double acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < spp; ++k) {  // sub-sample k of pixel p at k * npix + p (k_combine)
-        double s[12];
-        tri_load(sample_col, (int64_t)k * npix + p, s);
-        for (int c = 0; c < 12; ++c) acc[c] += s[c];
+// A block handles 64 pixels with nine waves, wave f summing column f (one of the nine A/D/S channels) of its
+// pixels, one lane per pixel, in sub-sample order. A pixel's samples are one contiguous run per column (k_combine
+// stores in sample order), so each wave stages kResolveChunk samples of its 64 pixels through LDS: every wave load
+// instruction reads 8 whole 64-byte runs instead of touching 64 lines for 8 bytes each. Nine waves per 64 pixels
+// keep enough loads in flight for a batch of only 32 768 pixels (the headline batch) to fill the chip.
+constexpr int kResolveChunk = 8;
+constexpr int kResolveBlock = 64 * 9;
+__global__ void __launch_bounds__(kResolveBlock) k_resolve(Cols<Tri9> sample_col, int64_t npix, int32_t spp,
+                                                           double* __restrict__ out) {
+    __shared__ double stage[9][64 * (kResolveChunk + 1)];
+    __shared__ double sum[9][64];
+    const int lane = threadIdx.x & 63, f = threadIdx.x >> 6;
+    double* st = stage[f];
+    const int64_t p0 = (int64_t)blockIdx.x * 64;  // the block's first pixel
+    const int64_t nsamp = npix * spp;
+    const uint64_t* col = sample_col.w + (int64_t)f * sample_col.cap;
+    double acc = 0.0;
+    for (int kb = 0; kb < spp; kb += kResolveChunk) {
+        const int kc = min(kResolveChunk, spp - kb);
+#pragma unroll
+        for (int m = 0; m < kResolveChunk; ++m) {  // element e: pixel e / kResolveChunk, sample kb + e % kResolveChunk
+            const int e = lane + 64 * m, lp = e / kResolveChunk, kk = e % kResolveChunk;
+            const int64_t si = (p0 + lp) * spp + kb + kk;
+            if (kk < kc && si < nsamp) st[lp * (kResolveChunk + 1) + kk] = __longlong_as_double(col[si]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int kk = 0; kk < kc; ++kk) acc += st[lane * (kResolveChunk + 1) + kk];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const double total = (double)spp;
-    for (int c = 0; c < 12; ++c) acc[c] *= 1.0 / total;
+    sum[f][lane] = acc * (1.0 / (double)spp);
+    __syncthreads();
+    const int64_t p = p0 + lane;
+    if (f >= 4 || p >= npix) return;
     double* o = out + 4 * p;
-    for (int k = 0; k < 3; ++k) {
-        double v = 0.0 + acc[k];
-        v += acc[4 + k];
-        v += acc[8 + k];
-        v *= 1.0 / 3.0;
-        o[k] = v;
+    if (f == 3) {
+        o[3] = 0.0;
+        return;
     }
-    o[3] = 0.0;
+    double v = 0.0 + sum[f][lane];  // (A + D + S) / 3 of channel f
+    v += sum[3 + f][lane];
+    v += sum[6 + f][lane];
+    v *= 1.0 / 3.0;
+    o[f] = v;
 }
 
 
@@ -2483,7 +2509,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
     const int64_t npix = nrows * hs;
     const int32_t spp = (int32_t)(h->S.cam.usteps * h->S.cam.vsteps);
     if (spp <= 0) return fail("render: usteps*vsteps must be positive");
-    int64_t batch = P->batch_samples > 0 ? P->batch_samples : (int64_t)1 << 21;
+    int64_t batch = P->batch_samples > 0 ? P->batch_samples : (int64_t)1 << 23;  // 8 M samples: tools/ab_batch.sh (2 M 219.6, 4 M 212.4, 8 M 208.4, 16 M 207.8 ms headline)
     int64_t pix_per_batch = std::max<int64_t>(1, batch / spp);
     const int path = h->S.cfg.path_length;
     if (st) {
@@ -2642,7 +2668,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         }
         {
             KTimer t(h, st, 4);
-            hipLaunchKernelGGL(k_resolve, dim3(grid_for(bp)), dim3(kBlock), 0, h->stream, h->sample_col, bp, spp,
+            hipLaunchKernelGGL(k_resolve, dim3((unsigned)((bp + 63) / 64)), dim3(kResolveBlock), 0, h->stream, h->sample_col, bp, spp,
                                dev_out + 4 * p0);
             FRT_HIP(hipGetLastError());
         }
