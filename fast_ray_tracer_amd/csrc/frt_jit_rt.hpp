@@ -529,6 +529,51 @@ __device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w)
     return ok && miss && w.omax < 1e8f * nd.sph[3];
 }
 
+// a round sphere the beam may meet (a top-level leaf of the pair kernel's walk):
+//  1  every ray of the beam hits it with its first root in (0, distance): the walk stops there, blocked
+//     (leaf_top: entries, stop_here, blocked)
+//  2  every root any ray can have lies before the ray's light point: the sphere can only stop the walk
+//     blocked or leave it going (the caller goes on and keeps the pair only if the rest ends blocked)
+//  0  neither is certain
+// v = C~ - O~ stands for a = C - O (true centre and origin) within ea per axis (the centre's binary32
+// rounding 2u (|C~| + R'), the origin's u max|o|, the subtraction's u |v|), 1.75 ea in the 2-norm;
+// R' = nd.sph[3] >= R >= R' (1 - 1e-5). The reference's binary64 roots err by far less than the
+// margins below (~1e-8 relative even at a tangent).
+//  * before the light: any root t <= |a| + R <= |v| (1 + 4u) + 1.75 ea + R' < Dnmin (1 - 1e-5) <= |D|.
+//  * hit: O outside, |a| >= |v| (1 - 4u) - 1.75 ea > 1.01 R'; every D in the beam's box lies in the
+//    cone about v of half-angle asin(Rc / |v|), Rc = R' (1 - 1e-5) (1 - 1e-4) - 1.75 ea (the cone is
+//    convex: its 8 corners decide, with a 1e-4 relative slack over their binary32 dot products), so each
+//    line passes the true centre closer than R (1 - 1e-4): two roots, the first in (0, |a|], |a| < |D|.
+__device__ __forceinline__ int sphere_beam32(const Node32& nd, const Beam32& w) {
+    float v[3], vv = 0.0f, vm = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        v[a] = nd.sph[a] - w.o[a];
+        vv = fmaf(v[a], v[a], vv);
+        vm = fmaxf(vm, fabsf(v[a]));
+    }
+    const float ea = 1.75f * fmaf(2.0f * kU, nd.sphc + nd.sph[3], kU * (w.omax + vm));
+    const float vn = sqrtf(vv);
+    const float Rp = nd.sph[3];
+    const float near_hi = fmaf(vn, 1.0f + 4.0f * kU, ea);  // >= |a|
+    const float lim = w.Dnmin * (1.0f - 1e-5f);
+    const bool before = near_hi + Rp < lim && vm < 1e4f * Rp && w.omax < 1e8f * Rp;
+    if (!before) return 0;
+    const float Rc = fmaf(Rp, (1.0f - 1e-5f) * (1.0f - 1e-4f), -ea);
+    bool hit = fmaf(vn, 1.0f - 4.0f * kU, -ea) > 1.01f * Rp && near_hi < lim && Rc > 0.0f;
+    const float k2 = (vv - Rc * Rc) * (1.0f + 1e-4f);  // |v|^2 cos^2 of the half-angle
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float d0 = (j & 1) ? w.Dhi[0] : w.Dlo[0];
+        const float d1 = (j & 2) ? w.Dhi[1] : w.Dlo[1];
+        const float d2 = (j & 4) ? w.Dhi[2] : w.Dlo[2];
+        const float dv = fmaf(d0, v[0], fmaf(d1, v[1], d2 * v[2]));
+        const float dd = fmaf(d0, d0, fmaf(d1, d1, d2 * d2));
+        hit = hit && dv > 0.0f && dv * dv > dd * k2;
+    }
+    return hit ? 1 : 2;
+}
+
 // the slab entries tmin / tmax as intervals; false when |d_a| may be below EPSILON
 __device__ __forceinline__ bool slab_iv(const F32& f, const float* lo, const float* hi, float bmax, Iv& tmin,
                                         Iv& tmax) {
