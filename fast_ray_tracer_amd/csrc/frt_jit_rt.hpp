@@ -700,6 +700,40 @@ __device__ __forceinline__ void cube_top32(const Node32& nd, const W& w, const I
     }
 }
 
+// (pair kernel) an axis-aligned cube wholly before every light point of the beam: each entry t of each
+// ray lies on the cube's surface (|t| <= the farthest corner's distance F from the origin; the EPSILON
+// branch moves it by < 1e-5 |t|), so any entry > 0 is also < |D|. The world box is the node's slab planes
+// (binary32, within u aabmax, remnants sigma (|o| + F)); o~ within u |o| per axis; 1.75 > sqrt(3).
+template <int kAa>
+__device__ __forceinline__ bool cube_before_light(const Node32& nd, const Beam32& w) {
+    if (kAa == 0) return false;
+    float f2 = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float m = fmaxf(fabsf(nd.aab[a] - w.o[a]), fabsf(nd.aab[a + 3] - w.o[a]));
+        f2 = fmaf(m, m, f2);
+    }
+    const float F = sqrtf(f2) * (1.0f + 8.0f * kU);
+    const float e = 1.75f * kU * (2.0f * nd.aabmax + 2.0f * w.omax) + nd.aasig * (w.omax + F) * 1.75f;
+    return (F + e) * (1.0f + 1e-4f) < w.Dnmin * (1.0f - 1e-5f);
+}
+
+// (pair kernel) cube_top32, but a cube the beam cannot decide that lies wholly before the light and casts
+// shadows can only stop the walk blocked or leave it going: the lane goes on marked ms (maybe blocked)
+template <int kAa>
+__device__ __forceinline__ void cube_top32_beam(const Node32& nd, const Beam32& w, const Iv& dist, bool act,
+                                                bool& alive, int& result, bool& any_entry, bool& amb, bool& ms) {
+    bool undecided = false;
+    cube_top32<kAa>(nd, w, dist, act, alive, result, any_entry, undecided);
+    if (!undecided) return;
+    if (nd.casts && cube_before_light<kAa>(nd, w)) {
+        ms = true;
+        alive = true;  // (act: the lane was alive)
+    } else {
+        amb = true;
+    }
+}
+
 // sorted entries of a non-cube leaf inside a CSG unit, exactly (binary64 ray of its parent frame)
 template <int kType, bool kXf>
 __device__ __forceinline__ void leaf_slots_iv(const DevScene& S, const WalkNode& nd, const Ray& R, bool act, Iv& t0,
