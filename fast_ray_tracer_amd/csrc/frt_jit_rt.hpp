@@ -441,6 +441,30 @@ __device__ __forceinline__ void beam32(const double* op, const float* pl, const 
 //    N0 / M+ and mx = N1 / D_a >= N1 / M+ (M+ = max D_a), rays with D_a < 0 have mn <= -N1 / M- and
 //    mx >= -N0 / M- (M- = max -D_a). Remnants: numerators shrink by sigma |o|, denominators grow by
 //    sigma |D|.
+//  * an origin strictly outside the slab (beam_axis_split): a ray moving away from it has a wholly negative
+//    s range on this axis (or, below EPSILON, no range: numerators of one sign times infinity), a ray moving
+//    towards it enters the slab at s >= snear = (distance to the near plane - rs) / (max |D_a| towards it);
+//    aa_slab turns that into a certain miss when another axis certainly enters at s >= 0 (the away rays:
+//    tmin >= 0 > tmax) and snear lies beyond every exit bound of the decided axes (the towards rays).
+template <bool kSig>
+__device__ __forceinline__ bool beam_axis_split(float thr, float bmax, float sig, const Beam32& w, int a, float B0,
+                                                float B1, float& snear) {
+    const float N0 = fminf(B0, B1) - w.o[a], N1 = fmaxf(B0, B1) - w.o[a];
+    const float eN = fmaf(1.01f * kU, bmax + fabsf(w.o[a]), kU * fmaxf(fabsf(N0), fabsf(N1)));
+    const float rs = eN + (kSig ? 1.01f * sig * w.omax : 0.0f);
+    const float ds = kSig ? 1.01f * sig * w.Dn : 0.0f;
+    const float f = 1.0f - 8.0f * kU;
+    if (N0 - rs > 0.0f) {  // below the slab: D_a > 0 moves towards it
+        snear = (N0 - rs) / (fmaxf(w.Dhi[a], 0.0f) + ds) * f;  // (x / 0 = +inf: no ray moves towards it)
+        return snear > 0.0f;
+    }
+    if (-N1 - rs > 0.0f) {  // above
+        snear = (-N1 - rs) / (fmaxf(-w.Dlo[a], 0.0f) + ds) * f;
+        return snear > 0.0f;
+    }
+    return false;
+}
+
 template <bool kSig>
 __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, const Beam32& w, int a, float B0, float B1,
                                           Iv& mn, Iv& mx) {
@@ -471,11 +495,23 @@ __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, cons
 
 template <bool kSig>
 __device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& tmin, Iv& tmax) {
-    bool ok = true;
+    bool ok = true, split_ok = true, any_ok = false;
+    float snear = 0.0f;  // max over the split axes
+    Iv smin{-__builtin_huge_valf(), -__builtin_huge_valf()}, smax{__builtin_huge_valf(), __builtin_huge_valf()};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         Iv mn, mx;
-        ok = beam_axis<kSig>(nd.aathr[a], nd.aabmax, nd.aasig, w, a, nd.aab[a], nd.aab[a + 3], mn, mx) && ok;
+        const bool oka = beam_axis<kSig>(nd.aathr[a], nd.aabmax, nd.aasig, w, a, nd.aab[a], nd.aab[a + 3], mn, mx);
+        ok = oka && ok;
+        if (oka) {  // the decided axes alone
+            smin = Iv{fmaxf(smin.lo, mn.lo), fmaxf(smin.hi, mn.hi)};
+            smax = Iv{fminf(smax.lo, mx.lo), fminf(smax.hi, mx.hi)};
+            any_ok = true;
+        } else {
+            float sn = 0.0f;
+            split_ok = beam_axis_split<kSig>(nd.aathr[a], nd.aabmax, nd.aasig, w, a, nd.aab[a], nd.aab[a + 3], sn) && split_ok;
+            snear = fmaxf(snear, sn);
+        }
         if (a == 0) {
             tmin = mn;
             tmax = mx;
@@ -483,6 +519,11 @@ __device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& t
             tmin = Iv{fmaxf(tmin.lo, mn.lo), fmaxf(tmin.hi, mn.hi)};
             tmax = Iv{fminf(tmax.lo, mx.lo), fminf(tmax.hi, mx.hi)};
         }
+    }
+    if (!ok && split_ok && any_ok && smin.lo >= 0.0f && snear > smax.hi) {  // a certain miss (beam_axis_split)
+        tmin = Iv{1.0f, 1.0f};
+        tmax = Iv{0.0f, 0.0f};
+        return true;
     }
     return ok;
 }
