@@ -493,15 +493,18 @@ __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, cons
     return ok;
 }
 
+// the three slabs [B0_a, B1_a] of a world box on the beam (beam_axis per axis, beam_axis_split's certain
+// misses); thr: the EPSILON thresholds, bmax >= |B|, sig: the permutation remnants (kSig)
 template <bool kSig>
-__device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& tmin, Iv& tmax) {
+__device__ __forceinline__ bool beam_slabs(const float* thr, float bmax, float sig, const Beam32& w, const float* B0,
+                                           const float* B1, Iv& tmin, Iv& tmax) {
     bool ok = true, split_ok = true, any_ok = false;
     float snear = 0.0f;  // max over the split axes
     Iv smin{-__builtin_huge_valf(), -__builtin_huge_valf()}, smax{__builtin_huge_valf(), __builtin_huge_valf()};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         Iv mn, mx;
-        const bool oka = beam_axis<kSig>(nd.aathr[a], nd.aabmax, nd.aasig, w, a, nd.aab[a], nd.aab[a + 3], mn, mx);
+        const bool oka = beam_axis<kSig>(thr[a], bmax, sig, w, a, B0[a], B1[a], mn, mx);
         ok = oka && ok;
         if (oka) {  // the decided axes alone
             smin = Iv{fmaxf(smin.lo, mn.lo), fmaxf(smin.hi, mn.hi)};
@@ -509,7 +512,7 @@ __device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& t
             any_ok = true;
         } else {
             float sn = 0.0f;
-            split_ok = beam_axis_split<kSig>(nd.aathr[a], nd.aabmax, nd.aasig, w, a, nd.aab[a], nd.aab[a + 3], sn) && split_ok;
+            split_ok = beam_axis_split<kSig>(thr[a], bmax, sig, w, a, B0[a], B1[a], sn) && split_ok;
             snear = fmaxf(snear, sn);
         }
         if (a == 0) {
@@ -526,6 +529,11 @@ __device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& t
         return true;
     }
     return ok;
+}
+
+template <bool kSig>
+__device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& tmin, Iv& tmax) {
+    return beam_slabs<kSig>(nd.aathr, nd.aabmax, nd.aasig, w, nd.aab, nd.aab + 3, tmin, tmax);
 }
 
 // frames that are not axis-aligned take no beam decision (their pairs are mixed)
@@ -549,25 +557,20 @@ __device__ __forceinline__ bool behind_all(const Iv& tmax, const Beam32& w) {
 // 1e-6 R') with R' = nd.sph[3] >= R (1 + 1e-6), holds the ball of radius R (1 + 1e-6) around the true
 // centre, so each line passes the centre at more than that (sphere_miss32's margin argument)
 __device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w) {
-    bool miss = false, ok = true;
-    Iv tmin{0.0f, 0.0f}, tmax{0.0f, 0.0f};
+    // (the line misses the box: a direction component of 0 keeps the line out of a slab its origin is outside)
     const float h = nd.sph[3] + fmaf(2.0f * kU, nd.sphc + nd.sph[3], 1e-6f * nd.sph[3]);
+    const float thr[3] = {0.0f, 0.0f, 0.0f};
+    float B0[3], B1[3];
+    bool near = true;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        Iv mn, mx;
-        const float B0 = nd.sph[a] - h, B1 = nd.sph[a] + h;
-        ok = beam_axis<false>(0.0f, nd.sphc + h, 0.0f, w, a, B0, B1, mn, mx) && ok;
-        if (a == 0) {
-            tmin = mn;
-            tmax = mx;
-        } else {
-            tmin = Iv{fmaxf(tmin.lo, mn.lo), fmaxf(tmin.hi, mn.hi)};
-            tmax = Iv{fminf(tmax.lo, mx.lo), fminf(tmax.hi, mx.hi)};
-        }
-        ok = ok && fabsf(w.o[a] - nd.sph[a]) < 1e4f * nd.sph[3];
+        B0[a] = nd.sph[a] - h;
+        B1[a] = nd.sph[a] + h;
+        near = near && fabsf(w.o[a] - nd.sph[a]) < 1e4f * nd.sph[3];
     }
-    miss = tmin.lo > tmax.hi;
-    return ok && miss && w.omax < 1e8f * nd.sph[3];
+    Iv tmin, tmax;
+    const bool ok = beam_slabs<false>(thr, nd.sphc + h, 0.0f, w, B0, B1, tmin, tmax);
+    return ok && near && tmin.lo > tmax.hi && w.omax < 1e8f * nd.sph[3];
 }
 
 // a round sphere the beam may meet (a top-level leaf of the pair kernel's walk):
