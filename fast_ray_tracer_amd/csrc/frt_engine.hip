@@ -1732,6 +1732,10 @@ void frt_scene_release(frt_scene_handle* h) {
                 if (c[2048 + 2 * k])
                     std::fprintf(stderr, "frt jit stats: node %d: %llu waves, %llu lanes tested; composites: %llu waves, %llu lanes entered\n",
                                  k, c[2048 + 2 * k], c[2048 + 2 * k + 1], c[3072 + 2 * k], c[3072 + 2 * k + 1]);
+            for (int k = std::max(h->S.num_nodes, 100); k < 512; ++k)  // the pair kernel's decision sites (frt_jit.hip)
+                if (c[3072 + 2 * k + 1])
+                    std::fprintf(stderr, "frt jit stats: beam site %d: %llu waves, %llu lanes\n", k, c[3072 + 2 * k],
+                                 c[3072 + 2 * k + 1]);
         }
     }
     for (void* p : h->owned) hip_ignore(hipFree(p));
