@@ -1899,6 +1899,19 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         using frt::jit::kMixSegs;
         int64_t NP = 0;  // parts of frt_jit_part_size() samples per path node (frt_jit_beam)
         for (const auto& L : h->host_lights) NP += std::max(1, (L.num_samples + frt_jit_part_size() - 1) / frt_jit_part_size());
+        // the pair kernel's lane index is 32-bit: batches of more than 2^31 - 1 (node, part) pairs run
+        // as node ranges (the shadow kernels read a node's ShadowHead and write its counts only, so a
+        // range is the same pass over rec + off and counts + off * lights)
+        // (FRT_JIT_MAX_PAIRS lowers the limit: the tests split small batches this way)
+        const char* mp_env = std::getenv("FRT_JIT_MAX_PAIRS");
+        const long long mp = mp_env ? std::atoll(mp_env) : 0;
+        const int64_t kMaxPairs = mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : (int64_t)((1ll << 31) - 1);
+        if (n * NP > kMaxPairs) {
+            const int64_t per = std::max<int64_t>(1, kMaxPairs / NP);
+            for (int64_t off = 0; off < n; off += per)
+                launch_shadow(h, B, rec + off, std::min(per, n - off), counts + off * h->S.num_lights);
+            return;
+        }
         const int64_t npairs = n * NP;
         const int64_t nblocks = (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
         uint32_t segcap = h->jit_beam_on ? (uint32_t)(((nblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock)

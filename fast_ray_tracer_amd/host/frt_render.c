@@ -11,7 +11,8 @@
  * canvas (the reference has no error return).
  *
  * Environment knobs (main.c stays unchanged):
- *   FRT_DEVICES=<i,j,..>   devices to split the rows over (default: every visible GPU)
+ *   FRT_DEVICES=<i,j,..>   devices to split the rows over (default: every visible GPU, or the
+ *                          launcher's LOCAL_RANK alone; precedence below, render_devices)
  *   FRT_GPUS=<n>           devices 0..n-1;  FRT_DEVICE=<n>: that one device
  *   FRT_SEED=<u64>         counter-RNG seed for multi-row area-light caches
  *   FRT_STATS_OUT=<file>   write a JSON line of frame statistics
@@ -32,11 +33,20 @@
 #include "src/renderer/renderer.h"
 
 static char g_host_error[512];
+/* the last render_multi's failure ("" after a successful one): the canvas alone cannot say, a scene
+ * may render black */
+static char g_render_error[512];
 
 const char *
 frt_host_last_error(void)
 {
     return g_host_error;
+}
+
+const char *
+frt_render_multi_error(void)
+{
+    return g_render_error;
 }
 
 static int
@@ -107,12 +117,14 @@ write_stats(const char *path, const frt_frame_stats *st, Camera cam, size_t uste
 }
 
 /*
- * Devices render_multi uses, in order:
+ * Devices render_multi uses: the first of these that is set decides (the later ones are ignored)
  *   FRT_DEVICES=<i,j,...>  explicit list (a device may repeat: several handles on one GPU)
  *   FRT_GPUS=<n>           devices 0 .. n-1
+ *   FRT_DEVICE=<n>         that one device
+ *   LOCAL_RANK=<r>         (set by torchrun-style launchers: one process per GPU) device r mod visible
+ *                          alone, so processes sharing a node do not all take every GPU
  *   otherwise              every visible device (the reference's pool is sized by
  *                          threading.num_threads; here the unit of parallelism is a GPU)
- * FRT_DEVICE=<n> (round 1) selects one device.
  */
 #define FRT_MAX_RENDER_DEVICES 64
 
@@ -142,6 +154,8 @@ render_devices(int *dev, int cap, char *err, size_t errlen)
         }
     } else if (one != NULL && *one) {
         dev[n++] = atoi(one);
+    } else if (getenv("LOCAL_RANK") != NULL && *getenv("LOCAL_RANK") && visible > 0) {
+        dev[n++] = atoi(getenv("LOCAL_RANK")) % visible;
     } else {
         for (int i = 0; i < visible && n < cap; ++i) {
             dev[n++] = i;
@@ -219,13 +233,16 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     int dev[FRT_MAX_RENDER_DEVICES];
     char err[512];
     frt_scene fs;
+    g_render_error[0] = '\0';
     if (host_flatten(cam, w, usteps, vsteps, jitter, &fs)) {
         fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", g_host_error);
+        snprintf(g_render_error, sizeof(g_render_error), "%s", g_host_error);
         return c;
     }
     const int n = render_devices(dev, FRT_MAX_RENDER_DEVICES, err, sizeof(err));
     if (n < 0) {
         fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", err);
+        snprintf(g_render_error, sizeof(g_render_error), "%s", err);
         frt_flat_scene_free(&fs);
         return c;
     }
@@ -301,6 +318,7 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
         }
     } else {
         fprintf(stderr, "frt: render_multi failed: %s\n", err);
+        snprintf(g_render_error, sizeof(g_render_error), "%s", err[0] ? err : "failed");
     }
     for (int k = 0; jobs != NULL && k < n; ++k) {
         free(jobs[k].rows);

@@ -200,7 +200,8 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
     (incl. the scene-specialised kernel's compile), render over the selected devices
     (``FRT_DEVICES`` list, e.g. "0,0"; default every visible GPU), copy to the host canvas.
     Returns the (height, width, 4) canvas; render_multi's failures are logged by it and
-    leave the canvas zeroed, so a zero canvas here raises."""
+    leave the canvas zeroed (the reference has no error return); ``frt_render_multi_error``
+    (host/frt_render.c) names the failure, and it raises here."""
     lib = host_lib()
     vp = ctypes.c_void_p
     lib.render_multi.restype = vp
@@ -225,9 +226,22 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
         out = np.ctypeslib.as_array(ptr, shape=(scene.height, scene.width, 4)).copy()
     finally:
         lib.canvas_free(c)
-    if not out.any():
-        raise RuntimeError("frt: render_multi returned an empty canvas (see its stderr message)")
+    lib.frt_render_multi_error.restype = ctypes.c_char_p
+    err = lib.frt_render_multi_error()
+    if err:
+        raise RuntimeError("frt: render_multi failed: " + err.decode(errors="replace"))
     return out
+
+
+def jit_cache_stats() -> dict:
+    """Counters of the scene-specialised kernels' code-object cache (include/frt_device.h
+    frt_jit_cache_stats) since the library was loaded."""
+    lib = host_lib()
+    lib.frt_jit_cache_stats.restype = ctypes.c_int
+    lib.frt_jit_cache_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    out = (ctypes.c_int64 * 5)()
+    lib.frt_jit_cache_stats(out, 5)
+    return dict(zip(("compiles", "disk_hits", "disk_writes", "module_loads", "module_hits"), map(int, out)))
 
 
 def jit_check(scene: Scene) -> tuple[int, str, str]:

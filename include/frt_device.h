@@ -249,6 +249,15 @@ void frt_scene_release(frt_scene_handle *h);
  * the compiler log, `src` (may be NULL) the generated HIP source. */
 int frt_jit_check(const frt_scene *scene, char *log, size_t log_cap, char *src, size_t src_cap);
 
+/* Counters of the scene-specialised kernels' code-object cache since the library was loaded (no device
+ * needed): out[0] hiprtc compiles, out[1] code objects read from the on-disk cache, out[2] code objects
+ * written to it, out[3] modules loaded (one per device and scene source), out[4] uploads that found
+ * their device's module loaded already. A scene's kernels are compiled once per process (every device
+ * and handle shares the code object) and, through the on-disk cache (FRT_JIT_CACHE_DIR, default
+ * $XDG_CACHE_HOME/frt_jit or ~/.cache/frt_jit; FRT_JIT_CACHE=0 turns it off), once per machine.
+ * Writes min(n, 5) counters; returns 5. */
+int frt_jit_cache_stats(int64_t *out, int n);
+
 /* Photon map entry points (parity tests; no scene needed).
  * frt_pm_balance replaces pm_balance (reference src/libs/photon_map/pm.c:329-494): the balanced
  * kd-tree of n photons given in the reference's storage order (pos: 3 doubles each); heap_of[i] = the

@@ -137,6 +137,12 @@ SCENES = {
                         "gi": {"photon-count": 10000, "include-caustics": True, "include-final-gather": True,
                                "irradiance-estimate-num": 50, "irradiance-estimate-radius": 0.3,
                                "irradiance-estimate-cone-filter-k": 1.1}}),
+    # the shipped estimate parameters (cornell_box.yml:18-20: k = 200, radius 0.1, cone 1.0, caustics
+    # off) over a 250k-photon global map: dense enough that queries hold more than the device list's
+    # 768 photons in range (make_pm_fixture.py)
+    "pm_cornell_shipped_250k": ("scenes/cornell_box/cornell_box.yml",
+                                {"size": (4, 4), "steps": (1, 1), "threads": 1, "no_golden": True,
+                                 "gi": {"photon-count": 250000}}),
     # cfg4 stand-in (bounding_boxes: 6 dragons, BVH) at its 4x4 CMJ grid, small frame
     "bounding_boxes_100x125_4x4": ("scenes/bounding_boxes/bounding_boxes.yml",
                                    {"size": (100, 125), "steps": (4, 4)}),

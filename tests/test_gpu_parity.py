@@ -154,11 +154,63 @@ def test_render_multi_two_handles_on_one_device_bit_identical(built):
 
 def test_render_multi_failure_returns_zero_canvas(built):
     """The reference has no error return: a failing render_multi logs and returns a zeroed canvas
-     instead of exiting the process."""
-    from fast_ray_tracer_amd.runtime import render_multi
+     instead of exiting the process; frt_render_multi_error names the failure (a
+    canvas may be black without one)."""
+    import ctypes
+    from fast_ray_tracer_amd.runtime import host_lib, render_multi
     sc = load_scene("cornell_gi_nomaps_16")
-    with pytest.raises(RuntimeError, match="empty canvas"):
+    with pytest.raises(RuntimeError, match="render_multi failed: .*not supported"):
         render_multi(sc, devices="0")
+    lib = host_lib()
+    lib.frt_render_multi_error.restype = ctypes.c_char_p
+    render_multi(load_scene("checkered_sphere_200"), devices="0")
+    assert lib.frt_render_multi_error() == b""
+
+
+_JIT_CACHE_PROBE = r"""
+import json, os, sys, time
+sys.path.insert(0, {tests!r})
+from conftest import load_scene
+from fast_ray_tracer_amd.runtime import GpuRenderer, jit_cache_stats, render_multi
+sc = load_scene("cornell_direct_64_4x4")
+out = {{}}
+t = time.perf_counter(); render_multi(sc, devices="0,0"); out["cold_ms"] = 1e3 * (time.perf_counter() - t)
+out["after_render_multi"] = jit_cache_stats()
+t = time.perf_counter(); render_multi(sc, devices="0,0"); out["warm_ms"] = 1e3 * (time.perf_counter() - t)
+a, b = GpuRenderer(sc), GpuRenderer(sc)
+a.close(); b.close()
+out["after_handles"] = jit_cache_stats()
+print("JSON" + json.dumps(out))
+"""
+
+
+def test_jit_compiled_once_and_cached_on_disk(built, tmp_path):
+    """The scene-specialised kernels' code object is compiled once per process and shared by every
+    device and handle (frt_jit.hip frt_jit_compile): render_multi over two handles on device 0 and two
+    more scene handles compile once; a second process finds the code object in the on-disk cache and
+    compiles nothing, so its first render_multi costs about what a warm one does."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, FRT_JIT_CACHE_DIR=str(tmp_path / "co"), FRT_JIT="1")
+
+    def probe():
+        p = subprocess.run([sys.executable, "-c", _JIT_CACHE_PROBE.format(tests=here)], env=env, cwd=here,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("JSON")][-1][4:])
+
+    first = probe()
+    print("first process", first)
+    assert first["after_render_multi"]["compiles"] == 1 and first["after_render_multi"]["disk_writes"] == 1
+    assert first["after_render_multi"]["module_loads"] == 1  # one device: one module, the second handle hits it
+    assert first["after_handles"]["compiles"] == 1 and first["after_handles"]["module_loads"] == 1
+    assert os.listdir(tmp_path / "co")
+    second = probe()
+    print("second process", second)
+    assert second["after_handles"]["compiles"] == 0 and second["after_render_multi"]["disk_hits"] == 1
+    # a cold render_multi in a new process: no compile (generous bound: the first hipModuleLoadData and
+    # stream setup of the process)
+    assert second["cold_ms"] <= second["warm_ms"] + 150.0, second
 
 
 def test_gpu_matches_oracle_on_cfg4_rows(built):

@@ -80,6 +80,8 @@ def test_pair_kernel_equals_per_ray_walk(built, name):
     walk gives for every ray of the pair: the canvas with and without it, bit for bit."""
     img_b, st_b = _render(name, True, beam=True)
     img_r, st_r = _render(name, True, beam=False)
+    # the scene-specialised kernels ran (not the generic walk for both)
+    assert st_b.shadow_jit == 1 and st_r.shadow_jit == 1
     assert np.array_equal(img_b, img_r)
 
 
@@ -93,3 +95,19 @@ def test_pair_kernel_on_headline_rows(built):
         img_g, _ = _render("cornell_direct_1920x1080_8x8", False, row_begin=rows[0], row_end=rows[1])
         assert st_b.shadow_jit == 1
         assert np.array_equal(img_b, img_r) and np.array_equal(img_b, img_g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "cornell_shipped_48_4x4"])
+def test_pair_kernel_batches_split_by_node_range(built, name):
+    """The pair kernel's lane index is 32-bit: a batch with more than 2^31 - 1 (node, light part) pairs
+    runs as node ranges (frt_engine.hip launch_shadow). FRT_JIT_MAX_PAIRS lowers the limit so a small
+    frame takes that path: the canvas must stay bit-identical."""
+    img_a, st_a = _render(name, True, beam=True)
+    os.environ["FRT_JIT_MAX_PAIRS"] = "4099"
+    try:
+        img_b, st_b = _render(name, True, beam=True)
+    finally:
+        del os.environ["FRT_JIT_MAX_PAIRS"]
+    assert st_a.shadow_jit == 1 and st_b.shadow_jit == 1
+    assert np.array_equal(img_a, img_b)

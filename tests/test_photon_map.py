@@ -1,9 +1,15 @@
 """Photon map parity against the reference's own balanced maps and estimates.
 
-Fixture tests/golden/pm_cornell_10k.npz (tests/golden/make_pm_fixture.py): the two maps of the
-cornell box scene with 10k photons each (caustic, global) as the reference's pm_balance left them
+Fixtures (tests/golden/make_pm_fixture.py), each the reference's maps as its pm_balance left them
 (heap order, pm.c:329-494), their storage order before it, and 2400 seeded queries with the
-reference's pm_irradiance_estimate results (irradiance and photons used, pm.c:91-156).
+reference's pm_irradiance_estimate results (irradiance and photons used, pm.c:91-156):
+  * pm_cornell_10k.npz: the cornell box scene with 10k photons per map (caustic, global), radius 0.3,
+    k = 50, cone k 1.1;
+  * pm_cornell_shipped_250k.npz: the shipped estimate parameters (cornell_box.yml:18-20: k = 200,
+    radius 0.1, cone k 1.0, caustics off) over a 250k-photon global map, a third of the queries at the
+    densest photons: 560 queries hold more photons in range than the device's per-wave list (768), so
+    the list-overflow path of the device estimate (frt_gi.hpp: the filtered second scan, or the
+    re-scans when even that overflows) is compared with the reference.
 
 * CPU: the oracle's balance and both forms of its search (oracle/pm_oracle.py) reproduce the
   fixture; frt_pm_balance (the engine's balance, C ABI, host only) reproduces the heap order and the
@@ -21,13 +27,21 @@ import pytest
 
 from conftest import GOLDEN
 
-FIX = os.path.join(GOLDEN, "pm_cornell_10k.npz")
+FIXTURES = ["pm_cornell_10k", "pm_cornell_shipped_250k"]
+# the device's per-wave list of photons in range (frt_engine.hip kGatherEstCap)
+DEVICE_LIST_CAP = 768
 
 
-@pytest.fixture(scope="module")
-def fx():
-    z = np.load(FIX)
-    return {k: z[k] for k in z.files}
+@pytest.fixture(scope="module", params=FIXTURES)
+def fx(request):
+    z = np.load(os.path.join(GOLDEN, request.param + ".npz"))
+    d = {k: z[k] for k in z.files}
+    d["name"] = request.param
+    return d
+
+
+def maps_of(fx):
+    return [m for m in (0, 1) if len(fx["kd_%d" % m])]
 
 
 def stored_order(fx, m):
@@ -57,14 +71,23 @@ def test_fixture_shape(fx):
     assert fx["kd_0"].shape[1] == 9 and fx["kd_1"].shape[1] == 9
     assert len(fx["query_pos"]) == len(fx["irrad"]) == len(fx["found"]) == 2400
     radius, k, cone_k = fx["params"]
-    assert (radius, int(k), cone_k) == (0.3, 50, 1.1)
     # the fixture exercises both regimes: fewer than k photons in range and the heap
     assert (fx["found"] == int(k)).sum() > 300 and ((fx["found"] > 8) & (fx["found"] < int(k))).sum() > 100
+    if fx["name"] == "pm_cornell_10k":
+        assert (radius, int(k), cone_k) == (0.3, 50, 1.1)
+    else:
+        # the shipped parameters (cornell_box.yml:18-20), the global map only (caustics off)
+        assert (radius, int(k), cone_k) == (0.1, 200, 1.0)
+        assert maps_of(fx) == [1] and len(fx["kd_1"]) == 250001  # max_photons + 1 (pm_store)
+        # queries past the device list's capacity: the overflow path is compared with the reference
+        assert (fx["in_range"] > DEVICE_LIST_CAP).sum() >= 100 and (fx["in_range"] > 1500).sum() >= 10
 
 
 @pytest.mark.parametrize("m", [0, 1])
 def test_oracle_balance_matches_reference(fx, m):
     import pm_oracle
+    if m not in maps_of(fx):
+        pytest.skip("empty map")
     pos, _, _ = stored_order(fx, m)
     n = len(pos)
     pbal, plane = pm_oracle.balance(np.concatenate([np.zeros((1, 3)), pos]))
@@ -76,6 +99,8 @@ def test_oracle_balance_matches_reference(fx, m):
 
 @pytest.mark.parametrize("m", [0, 1])
 def test_engine_balance_matches_reference(built, fx, m):
+    if m not in maps_of(fx):
+        pytest.skip("empty map")
     lib = ctypes.CDLL(built.DEVICE_LIB)
     lib.frt_pm_balance.restype = ctypes.c_int
     lib.frt_pm_balance.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
@@ -105,11 +130,16 @@ DEVICE_RTOL = 1e-9
 def test_oracle_estimates_match_reference(fx, m):
     """Both forms of the search on a sample of the queries (pure Python: a sample keeps it fast)."""
     import pm_oracle
+    if m not in maps_of(fx):
+        pytest.skip("empty map")
     radius, k, cone_k = float(fx["params"][0]), int(fx["params"][1]), float(fx["params"][2])
     kd = heap_kd(fx, m)
     idx = np.nonzero(fx["query_map"] == m)[0]
-    # the queries where the heap's first overflow decides the result come first, then a spread
-    pick = list(idx[::12])
+    if fx["name"] == "pm_cornell_10k":
+        pick = list(idx[::12])
+    else:  # the densest queries (past the device list), then a spread
+        dense = idx[np.argsort(-fx["in_range"][idx], kind="stable")]
+        pick = list(dense[:8]) + list(idx[::80])
     for qi in pick:
         x, nrm = fx["query_pos"][qi], fx["query_normal"][qi]
         step = pm_oracle.locate(kd[:, 0:3], kd[:, 8], x, radius, k)
@@ -130,7 +160,7 @@ def test_device_estimates_match_reference(built, fx):
                                     ctypes.c_int32, ctypes.c_double, vp, vp]
     radius, k, cone_k = float(fx["params"][0]), int(fx["params"][1]), float(fx["params"][2])
     bad = []
-    for m in (0, 1):
+    for m in maps_of(fx):
         pos, power, d = stored_order(fx, m)
         idx = np.nonzero(fx["query_map"] == m)[0]
         q = np.ascontiguousarray(np.concatenate([fx["query_pos"][idx], fx["query_normal"][idx]], axis=1))
@@ -146,7 +176,7 @@ def test_device_estimates_match_reference(built, fx):
 
 
 @pytest.mark.gpu
-def test_device_estimate_edge_cases(built, fx):
+def test_device_estimate_edge_cases(built):
     """No photons, all photons at one point (ties), queries far from every photon, k above the count."""
     lib = ctypes.CDLL(built.DEVICE_LIB)
     lib.frt_pm_estimate.restype = ctypes.c_int
