@@ -54,7 +54,6 @@ ASSETS = os.path.join(GOLDEN, "assets")
 DEFAULT_SCENE = "cornell_direct_1920x1080_8x8"
 GI_SCENE = "cornell_gi_1920x1080_8x8"
 CPU_SAMPLE_SCENE = "cornell_direct_240x135_8x8"
-CPU_SAMPLE_THREADS = 16  # the GPU box's CPU share per GPU (the reference binary's thread-count)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 2 cycles (SIMD32; binary64
 # and transcendental instructions take 2-4x: profiles/r01_microbench_valu.txt) at the 2.4 GHz peak clock
@@ -99,32 +98,36 @@ def reference_rays(name: str):
 
 def cpu_baseline() -> dict | None:
     """The reference's own pthread render_multi on this host, on a bounded sample of the workload:
-    the same camera and scene at 240x135 (1/64 of the pixels, 8x8 CMJ), CPU_SAMPLE_THREADS threads.
+    the same camera and scene at 240x135 (1/64 of the pixels, 8x8 CMJ), threads = the CPU quota of this process (runtime.cpu_share).
     The binary is oracle/_ref/bin/<sample>: built from the reference's sources by oracle/build_ref.sh
     in the build container (a git-ignored artefact that travels with the working tree; no reference
     source is in the repo). Without it, the repository's own C restatement (oracle/, "port") is timed."""
+    from fast_ray_tracer_amd.runtime import cpu_share
     rays = reference_rays(CPU_SAMPLE_SCENE)
     exe = os.path.join(ROOT, "oracle", "_ref", "bin", CPU_SAMPLE_SCENE)
     host_cpus = os.cpu_count()
+    # the reference's pool sized to the CPUs this process may use: the cgroup quota of the GPU box (16 per
+    # GPU) while os.cpu_count() reports the whole machine (256); more threads than the quota only time-slice
+    threads = cpu_share()
     if os.path.exists(exe) and rays:
         stats = "/tmp/frt_bench_ref_stats_%d.json" % os.getpid()
         os.makedirs("/tmp/frt_golden/out", exist_ok=True)
         t0 = time.time()
-        proc = subprocess.run([exe], cwd=ASSETS, env=dict(os.environ, FRT_REF_STATS=stats), stdout=subprocess.DEVNULL,
-                              stderr=subprocess.PIPE, text=True, timeout=600)
+        proc = subprocess.run([exe], cwd=ASSETS, env=dict(os.environ, FRT_REF_STATS=stats, FRT_REF_THREADS=str(threads)),
+                              stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, timeout=600)
         if proc.returncode != 0:
             log("cpu_baseline: reference run failed:", proc.stderr[-500:])
             return None
         st = json.load(open(stats))
         secs = st["render_multi_seconds"]
         return {"value": round(rays / secs / 1e6, 4), "unit": "Mrays/s", "cores": int(st["threads"]),
-                "kind": "reference", "threads": int(st["threads"]), "host_cpus_visible": host_cpus,
-                "seconds": round(secs, 3), "wall_seconds": round(time.time() - t0, 3),
-                "sample": "%s: the reference's render_multi (pthread pool, %d threads) built from /root/reference "
-                          "sources by oracle/build_ref.sh, %dx%dx%d spp (the benchmark camera at 1/64 of the "
-                          "pixels), %d reference rays counted by the oracle"
-                          % (CPU_SAMPLE_SCENE, st["threads"], st["width"], st["height"], st["usteps"] * st["vsteps"],
-                             rays)}
+                "kind": "reference", "threads": int(st["threads"]), "cpu_quota": cpu_share(),
+                "host_cpus_visible": host_cpus, "seconds": round(secs, 3), "wall_seconds": round(time.time() - t0, 3),
+                "sample": "%s: the reference's render_multi (pthread pool, %d threads = this process's CPU quota of "
+                          "the %d CPUs the machine shows) built from /root/reference sources by oracle/build_ref.sh, "
+                          "%dx%dx%d spp (the benchmark camera at 1/64 of the pixels), %d reference rays counted by "
+                          "the oracle" % (CPU_SAMPLE_SCENE, st["threads"], host_cpus, st["width"], st["height"],
+                                          st["usteps"] * st["vsteps"], rays)}
     # checker leg only (never the GPU path): the oracle restatement on the same sample
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -132,13 +135,13 @@ def cpu_baseline() -> dict | None:
     from conftest import load_scene
     scene = load_scene(CPU_SAMPLE_SCENE)
     t0 = time.time()
-    _, st = oracle.render(scene, threads=CPU_SAMPLE_THREADS, stats=True)
+    _, st = oracle.render(scene, threads=threads, stats=True)
     secs = time.time() - t0
     total = int(st["primary_rays"] + st["secondary_rays"] + st["shadow_rays"])
-    return {"value": round(total / secs / 1e6, 4), "unit": "Mrays/s", "cores": CPU_SAMPLE_THREADS, "kind": "port",
-            "threads": CPU_SAMPLE_THREADS, "host_cpus_visible": host_cpus, "seconds": round(secs, 3),
+    return {"value": round(total / secs / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "threads": threads, "cpu_quota": cpu_share(), "host_cpus_visible": host_cpus, "seconds": round(secs, 3),
             "sample": "%s: oracle/ C restatement of the reference (reference build absent), %d threads, %d rays"
-                      % (CPU_SAMPLE_SCENE, CPU_SAMPLE_THREADS, total)}
+                      % (CPU_SAMPLE_SCENE, threads, total)}
 
 
 def latest_pmc(kernel: str, workload: str):
@@ -389,6 +392,7 @@ def main():
             "reference_equivalent_rays_per_frame": ref_rays,
             "reference_equivalent_mrays_s": round(ref_rays * args.steps / t_max / 1e6, 3) if ref_rays else None,
             "kernel_ms_per_frame": {k: round(v, 4) for k, v in kernel_ms.items()},
+            "sub_ms_per_frame": {k: round(v, 4) for k, v in d.get("sub_ms", {}).items()},
             "shadow_pass": {
                 "kernels_ms_per_frame": {k: round(v, 4) for k, v in d.get("sub_ms", {}).items()
                                          if k in ("frt_jit_beam", "frt_jit_shadow")},

@@ -447,13 +447,10 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow_redo(DevScene S, Batch B
     if (e) atomicOr(err, e);
 }
 
-// lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725)
-__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<NodeRec> rec, int64_t n,
-                                                  const int32_t* __restrict__ counts, Cols<Tri9> surface) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const NodeRec nr = rec.load(i);
-    if (nr.material < 0) return;
+// lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725): the
+// A, D, S triples of path node i into out (out[4k + c]: term k, channel c)
+__device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, const NodeRec& nr, int64_t i,
+                                           const int32_t* __restrict__ counts, double* out) {
     double sA[3] = {0, 0, 0}, sD[3] = {0, 0, 0}, sS[3] = {0, 0, 0};
     if (S.cfg.include_direct) {
         for (int li = 0; li < S.num_lights; ++li) {
@@ -530,12 +527,87 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<Node
             }
         }
     }
-    double out[12];
     for (int k = 0; k < 3; ++k) {
         out[k] = sA[k];
         out[4 + k] = sD[k];
         out[8 + k] = sS[k];
     }
+    out[3] = out[7] = out[11] = 0.0;
+}
+
+// the node's shading loops over light points: some light reaches it (a non-zero unshadowed count:
+// lighting_microfacet's `if (!feq(intensity, 0))`, renderer.c:909) and diffuse or highlights are on
+__device__ __forceinline__ bool shade_heavy(const DevScene& S, const int32_t* __restrict__ counts, int64_t i) {
+    if (!S.cfg.include_direct || !(S.cfg.include_diffuse || S.cfg.include_spec_highlight)) return false;
+    for (int li = 0; li < S.num_lights; ++li)
+        if (counts[i * S.num_lights + li] != 0) return true;
+    return false;
+}
+
+// Shading in two kernels: most path nodes of a frame see no light sample at all (cornell 1920x1080: 83 % of
+// the (node, light) pairs are wholly shadowed), and a wave runs its light-point loops whenever one lane
+// needs them. k_shade writes the nodes without light-point work (ambient only) and appends the others to
+// kShadeSegs segments of a list (one atomic per wave on its segment's line); k_shade_lit shades the
+// listed nodes with every lane busy.
+constexpr int kShadeSegs = 64;
+static_assert(kShadeSegs == jit::kMixSegs, "k_shade_lit reads its slots with jit::mix_slot");
+__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<NodeRec> rec, int64_t n,
+                                                  const int32_t* __restrict__ counts, Cols<Tri9> surface,
+                                                  uint32_t* __restrict__ lit, unsigned* __restrict__ lcount,
+                                                  uint32_t segcap) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool heavy = false, mine = false;
+    NodeRec nr{};
+    if (i < n) {
+        nr = rec.load(i);
+        mine = nr.material >= 0;
+        heavy = mine && lit != nullptr && shade_heavy(S, counts, i);
+    }
+    if (mine && !heavy) {
+        double out[12];
+        shade_node(S, B, nr, i, counts, out);
+        tri_store(surface, i, out);
+    }
+    if (lit != nullptr) {
+        const unsigned long long m = __ballot(heavy);
+        if (m) {
+            const int lane = threadIdx.x & 63;
+            const int seg = (int)(blockIdx.x % kShadeSegs);
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(lcount + seg * jit::kMixLine, (unsigned)__popcll(m));
+            base = __shfl(base, 0, 64);
+            const unsigned at = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
+            if (heavy) lit[(size_t)seg * segcap + at] = (uint32_t)i;  // (segcap: a whole segment's blocks fit)
+        }
+    }
+}
+
+// the listed nodes (k_shade); one lane each, the grid sized for every node of the level
+#ifndef FRT_SHADE_WAVES
+#define FRT_SHADE_WAVES 1
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_SHADE_WAVES, 8))) k_shade_lit(DevScene S, Batch B, Cols<NodeRec> rec,
+                                                      const int32_t* __restrict__ counts, Cols<Tri9> surface,
+                                                      const uint32_t* __restrict__ lit,
+                                                      const unsigned* __restrict__ lcount, uint32_t segcap) {
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    // the listed total: every lane reads one segment's count (uniform per wave)
+    const int lane = threadIdx.x & 63;
+    const unsigned c = lcount[lane * jit::kMixLine];
+    unsigned incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const unsigned total = __shfl(incl, 63, 64);
+    if (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) >= total) return;  // (whole waves)
+    const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
+    if (m >= total) return;
+    const int64_t i = (int64_t)lit[slot];
+    const NodeRec nr = rec.load(i);
+    double out[12];
+    shade_node(S, B, nr, i, counts, out);
     tri_store(surface, i, out);
 }
 
@@ -1031,6 +1103,9 @@ constexpr int kGatherWavesPerBlock = FRT_GATHER_WAVES_PER_BLOCK;
 #define FRT_GATHER_REQ_PER_WAVE 64
 #endif
 constexpr int kGatherReqPerWave = FRT_GATHER_REQ_PER_WAVE;
+// (Tried and measured slower on cornell_gi_480x270_8x8: requests radix-sorted by a Morton key of their point,
+// 1793 -> 1855 ms plus 20 ms of sorting, and with the blocks dealt to the XCDs in contiguous runs 2600 ms:
+// the dense regions then crowd onto one XCD. The estimate is bound by instruction issue, not by L2 misses.)
 __global__ void __launch_bounds__(64 * kGatherWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8)))
 k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col) {
     FRT_EST_LDS_W(lds, kGatherEstCap, kGatherWavesPerBlock);
@@ -1165,6 +1240,11 @@ struct frt_scene_handle {
     uint64_t rays_walked = 0;           // shadow rays walked one by one in this frame
     uint64_t pairs_walked = 0;          // (node, light part) pairs they belong to
     unsigned long long uniform_stats[3] = {0, 0, 0};  // FRT_JIT_STATS: (node, light) pairs all lit / all shadowed / mixed
+    // k_shade's list of nodes with light-point work (kShadeSegs segments) and its segment counters
+    uint32_t* shade_lit = nullptr;
+    int64_t shade_lit_cap = 0;
+    unsigned* shade_lcount = nullptr;
+    int64_t shade_lcount_cap = 0;
     unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks;
                                               // then {waves, lanes} per node (frt_jit_rt.hpp node_stat)
     // work buffers (grow on demand)
@@ -1768,6 +1848,8 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->sample_col.w));
     hip_ignore(hipFree(h->out_dev));
     hip_ignore(hipFree(h->counters));
+    hip_ignore(hipFree(h->shade_lit));
+    hip_ignore(hipFree(h->shade_lcount));
     hip_ignore(hipFree(h->err));
     for (hipEvent_t e : h->ev_pool) hip_ignore(hipEventDestroy(e));
     if (h->ev[0]) hip_ignore(hipEventDestroy(h->ev[0]));
@@ -2118,33 +2200,33 @@ static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t
     return 0;
 }
 
-// pm_store's direction bytes decoded by pm_photon_dir (pm.c:80-88, 288-300)
-static void quantized_dir(const double* d, double* out) {
+// pm_store's direction bytes (pm.c:288-300): theta, phi of a unit direction
+static void dir_bytes(const double* d, uint8_t* tp) {
     double at = std::acos(d[2]) * (256.0 / M_PI);
     int theta = std::isfinite(at) ? (int)at : 0;
     theta = theta > 255 ? 255 : theta;
     double ap = std::atan2(d[1], d[0]) * (256.0 / (2.0 * M_PI));
     int phi = std::isfinite(ap) ? (int)ap : 0;
     phi = phi > 255 ? 255 : (phi < 0 ? phi + 256 : phi);
-    theta &= 255;
-    phi &= 255;
-    // the decoded angles' sines and cosines, tabulated once (the same expressions per byte value)
-    struct Tables {
-        double st[256], ct[256], c2p[256], s2p[256];
-        Tables() {
-            for (int b = 0; b < 256; ++b) {
-                const double ta = (double)b * (1.0 / 256.0) * M_PI, pa = (double)b * (1.0 / 256.0) * M_PI;
-                st[b] = std::sin(ta);
-                ct[b] = std::cos(ta);
-                c2p[b] = std::cos(2.0 * pa);
-                s2p[b] = std::sin(2.0 * pa);
-            }
+    tp[0] = (uint8_t)(theta & 255);
+    tp[1] = (uint8_t)(phi & 255);
+}
+
+// pm_photon_dir's tables (pm.c:60-66), the same expressions per byte value: {sin theta, cos theta} and
+// {cos 2 phi, sin 2 phi} per byte
+static const std::vector<double>& dir_tables() {
+    static const std::vector<double> t = [] {
+        std::vector<double> v(1024);
+        for (int b = 0; b < 256; ++b) {
+            const double angle = (double)b * (1.0 / 256.0) * M_PI;
+            v[(size_t)(2 * b)] = std::sin(angle);
+            v[(size_t)(2 * b + 1)] = std::cos(angle);
+            v[(size_t)(512 + 2 * b)] = std::cos(2.0 * angle);
+            v[(size_t)(512 + 2 * b + 1)] = std::sin(2.0 * angle);
         }
-    };
-    static const Tables T;
-    out[0] = T.st[theta] * T.c2p[phi];
-    out[1] = T.st[theta] * T.s2p[phi];
-    out[2] = T.ct[theta];
+        return v;
+    }();
+    return t;
 }
 
 // ---- the reference's kd-tree (pm_balance, pm.c:329-494), restated ----
@@ -2252,13 +2334,14 @@ static void pm_balance_heap(const double* pos, int64_t n, std::vector<int32_t>& 
 constexpr double kMaxGridCells = (double)(1 << 24);
 
 // One photon map on the device from photons in the reference's storage order (positions, scaled powers,
-// pm_photon_dir directions): balanced as pm_balance would (heap index per photon, split planes), the
-// photons the reference's search reaches binned into the dense grid (frt_gi.hpp wave_scan_cells; cell
-// edge radius / 3, doubled while the grid would exceed kMaxGridCells; sorted by cell, x fastest, so a
-// row of cells is one contiguous range). One allocation per map: binary32 positions | 80-byte records
-// (binary64 position, power, direction, heap index) | cell starts | the kd-tree (binary64 position and
-// split plane per heap index: the traversal order of the estimate's selection).
-static int make_photon_map(int64_t n, const double* pos, const double* power, const double* dir,
+// the stored theta / phi direction bytes): balanced as pm_balance would (heap index per photon, split
+// planes), the photons the reference's search reaches binned into the dense grid (frt_gi.hpp
+// wave_scan_cells; cell edge radius / 3, doubled while the grid would exceed kMaxGridCells; sorted by
+// cell, x fastest, so a row of cells is one contiguous range). One allocation per map: binary32
+// positions | 80-byte records (binary64 position, power, pm_photon_dir of the direction bytes, heap
+// index) | cell starts | the kd-tree (binary64 position and split plane per heap index: the traversal
+// order of the estimate's selection).
+static int make_photon_map(int64_t n, const double* pos, const double* power, const uint8_t* tp,
                            double irradiance_radius, void** out_mem, frt::PhotonMapDev& M) {
     *out_mem = nullptr;
     M = frt::PhotonMapDev{};
@@ -2288,6 +2371,11 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
         const double v = e ? std::atof(e) : 3.0;
         return v >= 1.0 && v <= 16.0 ? v : 3.0;
     }();
+    static const double max_cells = [] {  // FRT_PM_MAX_CELLS_LOG2: the grid's cell budget (A/B experiments only)
+        const char* e = std::getenv("FRT_PM_MAX_CELLS_LOG2");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 10 && v <= 30 ? std::ldexp(1.0, v) : kMaxGridCells;
+    }();
     double cell = (irradiance_radius > 0 ? irradiance_radius : 1.0) / cell_div;
     int64_t dims[3];
     for (;;) {
@@ -2297,7 +2385,7 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
             dims[k] = d < 1e9 ? (int64_t)d : (int64_t)1e9;
             cells *= (double)dims[k];
         }
-        if (cells <= kMaxGridCells) break;
+        if (cells <= max_cells) break;
         cell *= 2.0;
     }
     for (int k = 0; k < 3; ++k) {
@@ -2322,6 +2410,7 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
     for (int64_t b = 0; b < ncells; ++b) start[(size_t)b + 1] += start[(size_t)b];
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
     const size_t np = (size_t)std::max<int64_t>(nr, 1);
+    const std::vector<double>& T = dir_tables();
     std::vector<float> pos4(np * 4, 0.0f);
     std::vector<double> rec(np * 10, 0.0), kd((size_t)(n + 1) * 4, 0.0);
     for (int64_t i = 0; i < n; ++i) {
@@ -2334,8 +2423,12 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
             pos4[(size_t)(4 * j + k)] = (float)pos[3 * i + k];
             rec[(size_t)(10 * j + k)] = pos[3 * i + k];
             rec[(size_t)(10 * j + 3 + k)] = power[3 * i + k];
-            rec[(size_t)(10 * j + 6 + k)] = dir[3 * i + k];
         }
+        // pm_photon_dir (pm.c:80-88): d = (sin theta cos 2 phi, sin theta sin 2 phi, cos theta)
+        const int th = tp[2 * i], ph = tp[2 * i + 1];
+        rec[(size_t)(10 * j + 6)] = T[(size_t)(2 * th)] * T[(size_t)(512 + 2 * ph)];
+        rec[(size_t)(10 * j + 7)] = T[(size_t)(2 * th)] * T[(size_t)(512 + 2 * ph + 1)];
+        rec[(size_t)(10 * j + 8)] = T[(size_t)(2 * th + 1)];
         const int64_t hb = hx;
         std::memcpy(&rec[(size_t)(10 * j + 9)], &hb, sizeof(hb));
     }
@@ -2356,12 +2449,12 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
 }
 
 static int upload_photon_map(frt_scene_handle* h, int m, int64_t n, const double* pos, const double* power,
-                             const double* dir, double irradiance_radius) {
+                             const uint8_t* tp, double irradiance_radius) {
     auto& G = h->gi;
     hip_ignore(hipFree(G.map_mem[m]));
     G.map_mem[m] = nullptr;
     frt::PhotonMapDev M{};
-    if (make_photon_map(n, pos, power, dir, irradiance_radius, &G.map_mem[m], M)) return -1;
+    if (make_photon_map(n, pos, power, tp, irradiance_radius, &G.map_mem[m], M)) return -1;
     h->S.pmaps[m] = M;
     G.photons[m] = (uint64_t)n;
     return 0;
@@ -2369,13 +2462,14 @@ static int upload_photon_map(frt_scene_handle* h, int m, int64_t n, const double
 
 static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::StoredPhoton>& ph, double scale) {
     const int64_t n = (int64_t)ph.size();
-    std::vector<double> pos((size_t)n * 3), power((size_t)n * 3), qdir((size_t)n * 3);
+    std::vector<double> pos((size_t)n * 3), power((size_t)n * 3);
+    std::vector<uint8_t> tp((size_t)n * 2);
     for (int64_t i = 0; i < n; ++i)
         for (int k = 0; k < 3; ++k) {
             pos[(size_t)(3 * i + k)] = ph[(size_t)i].pos[k];
             power[(size_t)(3 * i + k)] = ph[(size_t)i].power[k] * scale;  // pm_scale_photon_power
         }
-    // pm_photon_dir of every photon, on the host's cores (acos / atan2 per photon)
+    // pm_store's direction bytes of every photon, on the host's cores (acos / atan2 per photon)
     {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(), 16,
                                                                        n / 65536 + 1}));
@@ -2383,11 +2477,11 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
         for (int w = 0; w < nt; ++w)
             pool.emplace_back([&, w]() {
                 const int64_t i0 = n * w / nt, i1 = n * (w + 1) / nt;
-                for (int64_t i = i0; i < i1; ++i) quantized_dir(ph[(size_t)i].dir, qdir.data() + 3 * i);
+                for (int64_t i = i0; i < i1; ++i) dir_bytes(ph[(size_t)i].dir, tp.data() + 2 * i);
             });
         for (auto& th : pool) th.join();
     }
-    return upload_photon_map(h, m, n, pos.data(), power.data(), qdir.data(), h->S.cfg.irradiance_radius);
+    return upload_photon_map(h, m, n, pos.data(), power.data(), tp.data(), h->S.cfg.irradiance_radius);
 }
 
 // trace_photons for one render seed: caustic map 0, global map 1
@@ -2496,6 +2590,9 @@ static void dump_walk_stats(frt_scene_handle* h) {
                  c[frt::kDbgProf + 13], c[frt::kDbgProf + 14], c[frt::kDbgProf + 15], c[frt::kDbgProf + 16],
                  c[frt::kDbgProf + 17], c[frt::kDbgProf + 18], c[frt::kDbgProf + 19], c[frt::kDbgProf + 20],
                  c[frt::kDbgProf + 21], c[frt::kDbgProf + 22]);
+    std::fprintf(stderr, " reduce_tried=%llu reduce_fallback=%llu queries=%llu candidates_read=%llu records_read=%llu",
+                 c[frt::kDbgProf + 23], c[frt::kDbgProf + 24], c[frt::kDbgProf + 25], c[frt::kDbgProf + 27],
+                 c[frt::kDbgProf + 28]);
     std::fprintf(stderr, "\nprepare prof (cycles):");
     const char* qn[5] = {"ray", "hits_load", "prepare", "spawn", "stores"};
     for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s=%llu", qn[k], c[frt::kDbgProf + 8 + k]);
@@ -2636,8 +2733,22 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             }
             {
                 KTimer t(h, st, 2);
+                // (FRT_SHADE_SPLIT=0: one kernel for every node, A/B runs)
+                const char* split_env = std::getenv("FRT_SHADE_SPLIT");
+                const bool split = !(split_env && std::strcmp(split_env, "0") == 0);
+                const int64_t nblocks = grid_for(n);
+                const uint32_t segcap = (uint32_t)(((nblocks + kShadeSegs - 1) / kShadeSegs) * kBlock);
+                if (split && (grow(&h->shade_lit, h->shade_lit_cap, (int64_t)segcap * kShadeSegs) ||
+                              grow(&h->shade_lcount, h->shade_lcount_cap, (int64_t)kShadeSegs * jit::kMixLine)))
+                    return -1;
+                if (split)
+                    FRT_HIP(hipMemsetAsync(h->shade_lcount, 0, (size_t)kShadeSegs * jit::kMixLine * sizeof(unsigned),
+                                           h->stream));
                 hipLaunchKernelGGL(k_shade, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n, L.counts,
-                                   L.surface);
+                                   L.surface, split ? h->shade_lit : nullptr, h->shade_lcount, segcap);
+                if (split)
+                    hipLaunchKernelGGL(k_shade_lit, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec,
+                                       L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap);
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.use_gi) {
@@ -2760,11 +2871,11 @@ int frt_pm_balance(const double* pos, int64_t n, int32_t* heap_of, int8_t* plane
     return 0;
 }
 
-int frt_pm_estimate(int device, const double* pos, const double* power, const double* dir, int64_t n,
+int frt_pm_estimate(int device, const double* pos, const double* power, const uint8_t* theta_phi, int64_t n,
                     const double* queries, int64_t nq, double radius, int32_t k, double cone_k, double* irrad,
                     int64_t* found) {
     if (n < 0 || nq < 0 || k < 1 || !(radius > 0.0) || (nq > 0 && (!queries || !irrad || !found)) ||
-        (n > 0 && (!pos || !power || !dir)))
+        (n > 0 && (!pos || !power || !theta_phi)))
         return fail("frt_pm_estimate: bad arguments");
     if (nq == 0) return 0;
     FRT_HIP(hipSetDevice(device));
@@ -2772,7 +2883,7 @@ int frt_pm_estimate(int device, const double* pos, const double* power, const do
     frt::PhotonMapDev M{};
     double *dq = nullptr, *dirr = nullptr;
     int64_t* dfound = nullptr;
-    int rc = make_photon_map(n, pos, power, dir, radius, &mem, M);
+    int rc = make_photon_map(n, pos, power, theta_phi, radius, &mem, M);
     auto run = [&]() -> int {
         FRT_HIP(hipMalloc(&dq, (size_t)nq * 6 * sizeof(double)));
         FRT_HIP(hipMalloc(&dirr, (size_t)nq * 3 * sizeof(double)));

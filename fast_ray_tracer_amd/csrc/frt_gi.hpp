@@ -87,13 +87,36 @@ constexpr int kEstCap = 1024;
 constexpr unsigned kEstSel = 256;
 
 struct EstLds {
-    uint2* ent;       // cap: (squared distance bits, photon index) of the photons within the radius
+    uint2* ent;       // cap: (24-bit key of d^2 / r^2, photon index) of the photons within the radius
     unsigned* hist;   // 256
     unsigned* sel;    // kEstSel: the photons the sum pass certainly takes (their records load together)
     unsigned cap;
 };
 
 __device__ __forceinline__ int est_lane() { return (int)(threadIdx.x & 63); }
+
+// FRT_WALK_PROF builds: phase cycles and counters of the estimate (frt_engine.hip dump_walk_stats)
+#ifdef FRT_WALK_PROF
+#define EST_STAMP(k)                                                                      \
+    do {                                                                                  \
+        const unsigned long long t1_ = prof_stamp();                                      \
+        if (lane == 0 && prof) atomicAdd(prof + (k), t1_ - est_t0);                      \
+        est_t0 = t1_;                                                                     \
+    } while (0)
+#define EST_COUNT(k, v)                                   \
+    do {                                                  \
+        if (lane == 0 && prof) atomicAdd(prof + (k), (v)); \
+    } while (0)
+#define EST_LANES(k, pred)                                                          \
+    do {                                                                            \
+        const unsigned long long m_ = __ballot(pred);                              \
+        if (est_lane() == 0 && prof) atomicAdd(prof + (k), (unsigned long long)__popcll(m_)); \
+    } while (0)
+#else
+#define EST_STAMP(k)
+#define EST_COUNT(k, v)
+#define EST_LANES(k, pred)
+#endif
 
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v) {
     const int lane = est_lane();
@@ -139,8 +162,11 @@ __device__ __forceinline__ unsigned est_key(float d2, float inv_r2) {
 // chunk in uniform control flow; `in`: this lane's candidate exists and lies
 // within the radius. The visiting order (rows in (z, y) order, photons in grid
 // order) is the same in every pass.
-template <typename F>
-__device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const double* x, double r, float r2f, F&& f) {
+// probe(candidates): called once, before any photon is loaded, with the number of candidates when the rows
+// fit one round of 64 (the usual case); returning true abandons the scan (wave_scan_cells returns false).
+template <typename F, typename P>
+__device__ __forceinline__ bool wave_scan_cells(const PhotonMapDev& M, const double* x, double r, float r2f, F&& f,
+                                                P&& probe, unsigned long long* prof = nullptr) {
     const int lane = est_lane();
     const double ax = fmax(fmax(fabs(x[0]), fabs(x[1])), fabs(x[2]));
     const double re = r * (1.0 + 1e-5) + 0x1p-20 * ax;
@@ -154,7 +180,7 @@ __device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const dou
         lo[k] = (int)fmin(fmax(a, 0.0), top);
         hi[k] = (int)fmin(fmax(b, 0.0), top);
     }
-    if (!any) return;
+    if (!any) return true;
     const int ny = hi[1] - lo[1] + 1;
     const int nrows = ny * (hi[2] - lo[2] + 1);
     const float xf[3] = {(float)x[0], (float)x[1], (float)x[2]};
@@ -183,6 +209,7 @@ __device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const dou
         const unsigned excl = incl - (unsigned)cnt;
         const int32_t off = s - (int32_t)excl;  // candidate g of this row is photon off + g
         const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
+        if (nrows <= 64 && probe(total)) return false;
         // the row of each candidate: the non-empty rows are visited in order with scalar
         // reads of their start (no cross-lane permutes); cur_off = the row holding the
         // chunk's first candidate
@@ -217,6 +244,7 @@ __device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const dou
                 inc[c] = base + 64u * c + (unsigned)lane < total;
                 qc[c] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 if (inc[c]) qc[c] = reinterpret_cast<const float4*>(M.pos4)[pc[c]];
+                EST_LANES(14, inc[c]);  // (FRT_WALK_PROF: candidate positions read)
             }
 #pragma unroll
             for (int c = 0; c < kScanChunks; ++c) {
@@ -232,9 +260,19 @@ __device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const dou
             }
         }
     }
+    return true;
 }
 
-// one photon's 80-byte record (grid order): binary64 position, power, direction, heap index
+template <typename F>
+__device__ __forceinline__ void wave_scan_cells(const PhotonMapDev& M, const double* x, double r, float r2f, F&& f,
+                                                unsigned long long* prof = nullptr) {
+    wave_scan_cells(M, x, r, r2f, f, [](unsigned) { return false; }, prof);
+}
+
+// one photon's 80-byte record (grid order): binary64 position, power, pm_photon_dir of its direction
+// bytes, heap index. (A 32-byte record with a power palette and the direction tables was measured
+// slower: the estimate is bound by instruction issue, and the palette / table lookups cost more
+// instructions than the wider record's loads.)
 struct PhotonRec {
     double2 r[5];
     __device__ __forceinline__ double d2(const double* x) const {  // pm.c:188-193, the reference's order
@@ -255,6 +293,19 @@ __device__ __forceinline__ PhotonRec photon_rec(const PhotonMapDev& M, int32_t p
 #pragma unroll
     for (int j = 0; j < 5; ++j) o.r[j] = q[j];
     return o;
+}
+
+// the photon's power (pm_scale_photon_power'd)
+__device__ __forceinline__ void photon_power(const PhotonMapDev&, const PhotonRec& pr, int32_t, double* pw) {
+    pw[0] = pr.r[1].y;
+    pw[1] = pr.r[2].x;
+    pw[2] = pr.r[2].y;
+}
+
+// pm_photon_dir (pm.c:80-88) . normal < 0 in the reference's operation order (pm.c:134): the photon
+// arrives from the side the normal faces away from
+__device__ __forceinline__ bool photon_facing(const PhotonMapDev&, const PhotonRec& pr, const double* normal) {
+    return (pr.r[3].x * normal[0] + pr.r[3].y * normal[1] + pr.r[4].x * normal[2]) < 0.0;
 }
 
 // the binary64 squared distance alone (the first 32 bytes of the record)
@@ -318,21 +369,20 @@ __device__ __forceinline__ bool found_before_any(const double* __restrict__ kd, 
 
 __device__ __forceinline__ unsigned wave_and(bool v) { return __ballot(!v) == 0ull ? 1u : 0u; }
 
-#ifdef FRT_WALK_PROF
-#define EST_STAMP(k)                                                                      \
-    do {                                                                                  \
-        const unsigned long long t1_ = prof_stamp();                                      \
-        if (lane == 0 && prof) atomicAdd(prof + (k), t1_ - est_t0);                      \
-        est_t0 = t1_;                                                                     \
-    } while (0)
-#define EST_COUNT(k, v)                                   \
-    do {                                                  \
-        if (lane == 0 && prof) atomicAdd(prof + (k), (v)); \
-    } while (0)
-#else
-#define EST_STAMP(k)
-#define EST_COUNT(k, v)
-#endif
+// sqrt(x) for x >= 0 within a few ulps (v_rsq_f64 and two Newton steps): the cone filter's weights only
+// scale the sums (which run in another order than the reference's anyway); every decision of the
+// selection uses exact squared distances
+__device__ __forceinline__ double sqrt_w(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double s = x * y, h = 0.5 * y;
+    double r = fma(-s, s, x);
+    s = fma(r, h, s);
+    r = fma(-s, s, x);
+    s = fma(r, h, s);
+    return x > 0.0 ? s : 0.0;
+}
+
+
 
 // the digit of rank `need` (1-based) in a 256-bin histogram held 4 bins per lane: its bin, count, and
 // the entries in lower bins (wave-uniform results)
@@ -368,6 +418,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     unsigned long long est_t0 = prof_stamp();
 #endif
     const int lane = est_lane();
+    EST_COUNT(12, 1ull);
     const double r2 = max_dist * max_dist;
     // error bound of a binary32 squared distance against the reference's binary64 one, for points
     // within reach of the radius: each difference within eb = 1.01u (2A + 2r) (A = max|x| + r: the two
@@ -389,22 +440,86 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         }
         return in;
     };
+    // Dense queries take a reduced radius rho < max_dist: the k nearest and the (k+1)-th are all the
+    // selection needs (the rare full traversal-order check re-scans the whole radius), so when the grid's
+    // row counts (the probe of pass 1, before any photon is loaded) predict many more than k + 1 photons
+    // in range (photons lie on surfaces: the count within rho scales as rho^2), only the photons within
+    // rho are listed. Exactness: every photon whose binary32 d^2 is below rho^2 - tol lies within rho, so
+    // at least k + 1 of those mean d^2_(k+1) < rho^2 exactly; every photon with exact d^2 < rho^2 has
+    // binary32 d^2 below rho^2 + tol and is listed; and rho^2 + tol stays below the radius' certain
+    // threshold (lo_thr), so every listed photon is in range. Otherwise (too few, or the list overflows)
+    // the full pass 1 runs.
+    unsigned total = 0, count = 0;
+    bool listed = false, filtered = false;
+#ifndef FRT_EST_REDUCE_ALPHA
+#define FRT_EST_REDUCE_ALPHA 2.0  // rho^2 / r^2 = alpha (k + 1) / predicted count
+#endif
+#ifndef FRT_EST_REDUCE_MIN
+#define FRT_EST_REDUCE_MIN 3.0  // reduce when the predicted count exceeds min (k + 1)
+#endif
+#ifndef FRT_EST_CAND_RATIO
+#define FRT_EST_CAND_RATIO 0.45  // photons in range per candidate of the chord-clipped rows (surfaces)
+#endif
+    double rho2 = 0.0;
+    bool probing = true;
+    auto want_reduce = [&](unsigned cands) {
+        if (!(probing && k >= 8 && FRT_EST_REDUCE_ALPHA > 0.0)) return false;
+        const double t_est = FRT_EST_CAND_RATIO * (double)cands;
+        if (!(t_est > FRT_EST_REDUCE_MIN * (double)(k + 1))) return false;
+        rho2 = r2 * (FRT_EST_REDUCE_ALPHA * (double)(k + 1) / t_est);
+        return __double2float_ru(rho2 + tol) < lo_thr;
+    };
     // pass 1: the photons within the radius into the LDS list in scan order, and the histogram of their
     // keys' top byte (the radix selects' first digit)
-    for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
-    __builtin_amdgcn_wave_barrier();
-    unsigned total = 0;
-    wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) {
-        const bool in = in_range(p, cand, d2);
-        const unsigned long long m = __ballot(in);
-        if (in) {
-            const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
-            if (at < L.cap) L.ent[at] = make_uint2(__float_as_uint(d2), (unsigned)p);
-            atomicAdd(&L.hist[est_key(d2, inv_r2) >> 16], 1u);
+    auto pass1 = [&]() {
+        for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        total = 0;
+        const bool done = wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) {
+            const bool in = in_range(p, cand, d2);
+            const unsigned long long m = __ballot(in);
+            if (in) {
+                const unsigned at = total + (unsigned)__popcll(m & ((1ull << lane) - 1));
+                const unsigned key = est_key(d2, inv_r2);
+                if (at < L.cap) L.ent[at] = make_uint2(key, (unsigned)p);
+                atomicAdd(&L.hist[key >> 16], 1u);
+            }
+            total += (unsigned)__popcll(m);
+        }, want_reduce, prof);
+        __builtin_amdgcn_wave_barrier();
+        count = total;
+        listed = total <= L.cap;
+        return done;
+    };
+    if (!pass1()) {
+        const float rlo = __double2float_rd(rho2 - tol), rhi = __double2float_ru(rho2 + tol);
+        for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        unsigned n_in = 0, n_lo = 0;
+        wave_scan_cells(M, x, sqrt((double)rhi), rhi, [&](int32_t p, bool in, float d2) {
+            const unsigned long long m = __ballot(in);
+            if (in) {
+                const unsigned at = n_in + (unsigned)__popcll(m & ((1ull << lane) - 1));
+                const unsigned key = est_key(d2, inv_r2);
+                if (at < L.cap) L.ent[at] = make_uint2(key, (unsigned)p);
+                atomicAdd(&L.hist[key >> 16], 1u);
+            }
+            n_in += (unsigned)__popcll(m);
+            n_lo += (unsigned)__popcll(__ballot(in && d2 < rlo));
+        }, prof);
+        __builtin_amdgcn_wave_barrier();
+        const bool reduced = n_lo >= (unsigned)k + 1u && n_in <= L.cap;
+        EST_COUNT(10, 1ull);
+        EST_COUNT(11, reduced ? 0ull : 1ull);
+        if (reduced) {
+            total = n_in;  // (> k: found = k)
+            count = n_in;
+            listed = filtered = true;
+        } else {
+            probing = false;
+            pass1();
         }
-        total += (unsigned)__popcll(m);
-    });
-    __builtin_amdgcn_wave_barrier();
+    }
     EST_STAMP(0);
     const unsigned found = total < (unsigned)k ? total : (unsigned)k;
     if (found < 8) return found;
@@ -413,8 +528,6 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     // the list: every photon in range or, when they overflow the wave's LDS and the heap decides,
     // those whose key's top digit is at most one beyond the (k+1)-th's (which covers the band, dk <
     // 2^16), stored by a second scan; only the rare traversal-order check needs the others (re-scan)
-    unsigned count = total;
-    bool listed = total <= L.cap, filtered = false;
     if (!listed && total > (unsigned)k) {
         unsigned b1, c1, below1;
         radix_pick(h4, (unsigned)k + 1u, b1, c1, below1);
@@ -425,11 +538,12 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         if (n_le <= L.cap) {
             unsigned at0 = 0;
             wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) {
-                const bool keep = in_range(p, cand, d2) && (est_key(d2, inv_r2) >> 16) <= top;
+                const unsigned key = est_key(d2, inv_r2);
+                const bool keep = in_range(p, cand, d2) && (key >> 16) <= top;
                 const unsigned long long m = __ballot(keep);
-                if (keep) L.ent[at0 + (unsigned)__popcll(m & ((1ull << lane) - 1))] = make_uint2(__float_as_uint(d2), (unsigned)p);
+                if (keep) L.ent[at0 + (unsigned)__popcll(m & ((1ull << lane) - 1))] = make_uint2(key, (unsigned)p);
                 at0 += (unsigned)__popcll(m);
-            });
+            }, prof);
             __builtin_amdgcn_wave_barrier();
             count = at0;
             listed = filtered = true;
@@ -441,7 +555,9 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     // every pass visits the listed photons in the same order (the list, or a re-scan when unlisted);
     // visit_all also the ones a filtered list omits
     auto scan_all = [&](auto&& fn) {
-        wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) { fn(p, in_range(p, cand, d2), d2); });
+        wave_scan_cells(M, x, max_dist, hi_thr, [&](int32_t p, bool cand, float d2) {
+            fn(p, in_range(p, cand, d2), est_key(d2, inv_r2));
+        }, prof);
     };
     auto visit = [&](auto&& fn) {
         if (listed) {
@@ -449,7 +565,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                 const unsigned i = base + (unsigned)lane;
                 const bool in = i < count;
                 const uint2 e = in ? L.ent[i] : make_uint2(0u, 0u);
-                fn((int32_t)e.y, in, __uint_as_float(e.x));
+                fn((int32_t)e.y, in, e.x);
             }
         } else {
             scan_all(fn);
@@ -459,21 +575,26 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         if (filtered) scan_all(fn);
         else visit(fn);
     };
-    const double cone_r = cone_k * max_dist;
+    const double cone_r = cone_k * max_dist, inv_cone_r = 1.0 / cone_r;
     double acc[3] = {0.0, 0.0, 0.0};
-    auto photon_weighted = [&](const PhotonRec& pr, double dp, double* w) {  // pm.c:129-145
-        const double weight = 1.0 - dp / cone_r;
-        const bool facing = (pr.r[3].x * normal[0] + pr.r[3].y * normal[1] + pr.r[4].x * normal[2]) < 0.0;
-        w[0] = facing ? pr.r[1].y * weight : 0.0;
-        w[1] = facing ? pr.r[2].x * weight : 0.0;
-        w[2] = facing ? pr.r[2].y * weight : 0.0;
+    // pm.c:129-145 (weight = 1 - sqrt(dist2) / (k r), within a few ulps)
+    auto photon_weighted = [&](const PhotonRec& pr, int32_t p, double dp, double* w) {
+        const double weight = 1.0 - dp * inv_cone_r;
+        const bool facing = photon_facing(M, pr, normal);
+        double pw[3];
+        photon_power(M, pr, p, pw);
+        w[0] = facing ? pw[0] * weight : 0.0;
+        w[1] = facing ? pw[1] * weight : 0.0;
+        w[2] = facing ? pw[2] * weight : 0.0;
     };
-    auto accumulate = [&](const PhotonRec& pr, double dp) {
-        const double weight = 1.0 - dp / cone_r;
-        if ((pr.r[3].x * normal[0] + pr.r[3].y * normal[1] + pr.r[4].x * normal[2]) < 0.0) {
-            acc[0] += pr.r[1].y * weight;
-            acc[1] += pr.r[2].x * weight;
-            acc[2] += pr.r[2].y * weight;
+    auto accumulate = [&](const PhotonRec& pr, int32_t p, double dp) {
+        const double weight = 1.0 - dp * inv_cone_r;
+        if (photon_facing(M, pr, normal)) {
+            double pw[3];
+            photon_power(M, pr, p, pw);
+            acc[0] = fma(pw[0], weight, acc[0]);
+            acc[1] = fma(pw[1], weight, acc[1]);
+            acc[2] = fma(pw[2], weight, acc[2]);
         }
     };
     auto finish = [&](double d0) {
@@ -485,10 +606,11 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         irrad[2] *= tmp;
     };
     if (total <= (unsigned)k) {  // every photon in range: no heap, dist2[0] = max_dist^2
-        visit([&](int32_t p, bool in, float) {
+        visit([&](int32_t p, bool in, unsigned) {
+            EST_LANES(15, in);
             if (in) {
                 const PhotonRec pr = photon_rec(M, p);
-                accumulate(pr, sqrt(pr.d2(x)));
+                accumulate(pr, p, sqrt_w(pr.d2(x)));
             }
         });
         finish(r2);
@@ -515,8 +637,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                 for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
                 __builtin_amdgcn_wave_barrier();
                 const unsigned pf = prefix[s], mk = mask[s];
-                visit([&](int32_t, bool in, float d2) {
-                    const unsigned key = est_key(d2, inv_r2);
+                visit([&](int32_t, bool in, unsigned key) {
                     if (in && (key & mk) == pf) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
                 });
                 __builtin_amdgcn_wave_barrier();
@@ -537,8 +658,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     // pass B: photons with keys in [blo, bhi] set aside (up to 64, in L.hist), the certain ones counted
     // and the certain ones' indices compacted into L.sel (while they fit)
     unsigned c_in = 0, nb = 0;
-    visit([&](int32_t p, bool in, float d2) {
-        const unsigned key = est_key(d2, inv_r2);
+    visit([&](int32_t p, bool in, unsigned key) {
         const bool band = in && key >= blo && key <= bhi, cert = in && key < blo;
         const unsigned long long lt = (1ull << lane) - 1;
         const unsigned long long bm = __ballot(band), cm = __ballot(cert);
@@ -564,11 +684,13 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     const bool fast = nb <= 64u && need >= 1u && need + 1u <= nb;
     if (fast) {
         mine_band = (unsigned)lane < nb;
+        EST_LANES(15, mine_band);
         if (mine_band) {
-            const PhotonRec pr = photon_rec(M, (int32_t)L.hist[lane]);
+            const int32_t bp = (int32_t)L.hist[lane];
+            const PhotonRec pr = photon_rec(M, bp);
             bv = pr.d2(x);
             bh = pr.heap();
-            photon_weighted(pr, sqrt(bv), bw);
+            photon_weighted(pr, bp, sqrt_w(bv), bw);
         }
         for (unsigned j = 0; j < nb; ++j) {
             const double vj = readlane_dd(bv, (int)j);
@@ -588,8 +710,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
             for (int shift = 56; shift >= 0; shift -= 8) {
                 for (int j = 0; j < 4; ++j) L.hist[4 * lane + j] = 0u;
                 __builtin_amdgcn_wave_barrier();
-                visit([&](int32_t p, bool in, float d2) {
-                    const unsigned key = est_key(d2, inv_r2);
+                visit([&](int32_t p, bool in, unsigned key) {
                     const bool band = in && key >= blo && key <= bhi;
                     if (band) {
                         const unsigned long long b = (unsigned long long)__double_as_longlong(photon_d2(M, p, x));
@@ -609,8 +730,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         vk = exact_rank(need);
         vk1 = exact_rank(need + 1u);
         int32_t rh = 0;
-        visit([&](int32_t p, bool in, float d2) {  // the (k+1)-th's heap index (first of equal distances)
-            const unsigned key = est_key(d2, inv_r2);
+        visit([&](int32_t p, bool in, unsigned key) {  // the (k+1)-th's heap index (first of equal distances)
             int32_t hx = 0;
             if (in && key >= blo && key <= bhi && photon_d2(M, p, x) == vk1) hx = photon_heap(M, p);
             const unsigned long long hm = __ballot(hx != 0);
@@ -631,25 +751,27 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
             const unsigned i0 = base + (unsigned)lane, i1 = i0 + 64u;
             const bool a = i0 < c_in, b = i1 < c_in;
             PhotonRec ra, rb;
-            if (a) ra = photon_rec(M, (int32_t)L.sel[i0]);
-            if (b) rb = photon_rec(M, (int32_t)L.sel[i1]);
+            const int32_t pa = a ? (int32_t)L.sel[i0] : 0, pb = b ? (int32_t)L.sel[i1] : 0;
+            EST_LANES(15, a);
+            EST_LANES(15, b);
+            if (a) ra = photon_rec(M, pa);
+            if (b) rb = photon_rec(M, pb);
             if (a) {
-                accumulate(ra, sqrt(ra.d2(x)));
+                accumulate(ra, pa, sqrt_w(ra.d2(x)));
                 before_all = before_all && found_before(ra.heap(), R, qmask);
             }
             if (b) {
-                accumulate(rb, sqrt(rb.d2(x)));
+                accumulate(rb, pb, sqrt_w(rb.d2(x)));
                 before_all = before_all && found_before(rb.heap(), R, qmask);
             }
         }
     }
-    if (!compact || !fast) visit([&](int32_t p, bool in, float d2) {
-        const unsigned key = est_key(d2, inv_r2);
+    if (!compact || !fast) visit([&](int32_t p, bool in, unsigned key) {
         const bool certain = in && key < blo && !compact;
         const bool band = in && key >= blo && key <= bhi && !fast;
         if (certain) {
             const PhotonRec pr = photon_rec(M, p);
-            accumulate(pr, sqrt(pr.d2(x)));
+            accumulate(pr, p, sqrt_w(pr.d2(x)));
             before_all = before_all && found_before(pr.heap(), R, qmask);
         }
         if (__ballot(band)) {  // (slow path) band photons: membership by their binary64 distance
@@ -659,7 +781,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                 const double v = pr.d2(x);
                 nearer = v < vk;
                 // those at the k-th's and the (k+1)-th's distance are added after the check
-                if (nearer) accumulate(pr, sqrt(v));
+                if (nearer) accumulate(pr, p, sqrt_w(v));
                 if (v <= vk && pr.heap() != R) before_all = before_all && found_before(pr.heap(), R, qmask);
             }
             below_k += (unsigned)__popcll(__ballot(nearer));
@@ -676,8 +798,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         auto consider = [&](int32_t hx) {
             if (last == 0 || found_before_any(M.kd, last, hx, x)) last = hx;
         };
-        visit([&](int32_t p, bool in, float d2) {
-            const unsigned key = est_key(d2, inv_r2);
+        visit([&](int32_t p, bool in, unsigned key) {
             if (in && key < blo) consider(photon_heap(M, p));
             if (in && key >= blo && key <= bhi && !fast && photon_d2(M, p, x) <= vk) consider(photon_heap(M, p));
         });
@@ -690,8 +811,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         const int32_t Lh = __builtin_amdgcn_readlane(last, 0);
         const unsigned lmask = near_mask(M.kd, Lh, x);
         bool after = true;
-        visit_all([&](int32_t p, bool in, float d2) {
-            const unsigned key = est_key(d2, inv_r2);
+        visit_all([&](int32_t p, bool in, unsigned key) {
             bool other = in && key > bhi;
             if (in && key >= blo && key <= bhi && !fast) other = photon_d2(M, p, x) > vk;
             if (other) after = after && !found_before(photon_heap(M, p), Lh, lmask);
@@ -713,8 +833,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
             take_k -= 1;
             take_k1 = 1;
         }
-        visit([&](int32_t p, bool in, float d2) {
-            const unsigned key = est_key(d2, inv_r2);
+        visit([&](int32_t p, bool in, unsigned key) {
             const bool band = in && key >= blo && key <= bhi;
             if (__ballot(band)) {
                 double v = -1.0;
@@ -723,7 +842,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                 const unsigned long long below = (1ull << lane) - 1;
                 const unsigned long long mk = __ballot(ek), mk1 = __ballot(ek1);
                 if ((ek && (unsigned)__popcll(mk & below) < take_k) || (ek1 && (unsigned)__popcll(mk1 & below) < take_k1))
-                    accumulate(photon_rec(M, p), sqrt(v));
+                    accumulate(photon_rec(M, p), p, sqrt_w(v));
                 take_k -= min(take_k, (unsigned)__popcll(mk));
                 take_k1 -= min(take_k1, (unsigned)__popcll(mk1));
             }

@@ -188,8 +188,23 @@ __device__ __forceinline__ double pow_ns(double x, double y) {
     if (y >= 0.0 && y < 4096.0 && y == __builtin_floor(y)) {
         const unsigned e = (unsigned)y;
         double r = 1.0, b = x;
+        const unsigned e0 = (unsigned)__builtin_amdgcn_readfirstlane((int)e);
+        if (__ballot(e != e0) == 0ull) {
+            // one exponent in the whole wave (one material's Ns): a scalar loop over its bits, the same
+            // products in the same order as below, without the selects and the squarings past the top bit
+            for (unsigned k = 0; (e0 >> k) != 0u; ++k) {
+                if ((e0 >> k) & 1u) r = r * b;
+                b *= b;
+            }
+            return r;
+        }
+        // several exponents: every lane runs the squarings of the wave's largest one (uniform trip count)
+        unsigned emax = e;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {  // fixed trip count: no loop-carried divergence
+        for (int o = 32; o > 0; o >>= 1) emax = max(emax, (unsigned)__shfl_xor((int)emax, o, 64));
+        const unsigned bits = 32u - (unsigned)__clz((int)emax);
+#pragma nounroll
+        for (unsigned k = 0; k < bits; ++k) {
             r = (e >> k) & 1u ? r * b : r;
             b *= b;
         }

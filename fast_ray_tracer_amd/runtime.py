@@ -233,6 +233,20 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
     return out
 
 
+def cpu_share() -> int:
+    """The host CPUs this process may use: the cgroup's CPU quota (cpu.max) when one is set, else the
+    CPUs in its affinity mask. On the GPU box os.cpu_count() reports the whole machine (256) while the
+    quota per GPU is 16."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def jit_cache_stats() -> dict:
     """Counters of the scene-specialised kernels' code-object cache (include/frt_device.h
     frt_jit_cache_stats) since the library was loaded."""

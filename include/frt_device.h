@@ -264,11 +264,11 @@ int frt_jit_cache_stats(int64_t *out, int n);
  * heap index (1..n) of photon i, plane[h] (n + 1 entries) = the split axis of heap node h. Host only.
  * frt_pm_estimate replaces pm_irradiance_estimate (pm.c:91-156, with pm_locate_photons pm.c:163-252)
  * over one map balanced as above: nq queries (pos[3], normal[3] each) on `device`; irrad receives 3
- * doubles per query (before lighting_gi's scaling), found the photons used. pos / power / dir: 3
- * doubles per photon in storage order, power already scaled (pm_scale_photon_power), dir = pm_photon_dir
- * of the photon's theta / phi. */
+ * doubles per query (before lighting_gi's scaling), found the photons used. pos / power: 3 doubles per
+ * photon in storage order, power already scaled (pm_scale_photon_power); theta_phi: the photon's stored
+ * direction bytes (Photon.theta, Photon.phi, pm.c:288-300; decoded as pm_photon_dir does). */
 int frt_pm_balance(const double *pos, int64_t n, int32_t *heap_of, int8_t *plane);
-int frt_pm_estimate(int device, const double *pos, const double *power, const double *dir, int64_t n,
+int frt_pm_estimate(int device, const double *pos, const double *power, const uint8_t *theta_phi, int64_t n,
                     const double *queries, int64_t nq, double radius, int32_t k, double cone_k,
                     double *irrad, int64_t *found);
 

@@ -1262,10 +1262,10 @@ ray_for_pixel(Camera cam, size_t px, size_t py, const double *jit, oray *res)
 struct job {
     Camera cam;
     World w;
-    size_t usteps, vsteps, row_begin, row_end;
+    size_t usteps, vsteps, row_begin, row_end, row_stride;
     bool jitter;
     double *out;
-    atomic_size_t next_row;
+    atomic_size_t next_row; /* job index j: row row_begin + j * row_stride */
     pthread_mutex_t stats_lock;
     frt_oracle_stats stats;
 };
@@ -1287,7 +1287,8 @@ worker(void *arg)
     Camera cam = jb->cam;
     double total = (double)jb->usteps * (double)jb->vsteps;
     for (;;) {
-        size_t row = atomic_fetch_add(&jb->next_row, 1);
+        const size_t j = atomic_fetch_add(&jb->next_row, 1);
+        const size_t row = jb->row_begin + j * jb->row_stride;
         if (row >= jb->row_end) break;
         struct sampler smp; /* one table per row job (renderer.c:211) */
         sampler_2d(jb->jitter, jb->usteps, jb->vsteps, sampler_default_constraint, &smp);
@@ -1308,7 +1309,7 @@ worker(void *arg)
                 }
             }
             for (int k = 0; k < 12; ++k) acc[k] *= 1.0 / total;
-            double *o = jb->out + 4 * ((row - jb->row_begin) * cam->hsize + px);
+            double *o = jb->out + 4 * (j * cam->hsize + px);
             double pix[3];
             for (int k = 0; k < 3; ++k) {
                 pix[k] = 0.0 + acc[k];
@@ -1349,8 +1350,9 @@ warm_bounds(Shape s)
 }
 
 int
-frt_oracle_render_rows(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter,
-                       size_t row_begin, size_t row_end, int nthreads, double *out, frt_oracle_stats *stats)
+frt_oracle_render_rows_strided(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter,
+                               size_t row_begin, size_t row_end, size_t row_stride, int nthreads, double *out,
+                               frt_oracle_stats *stats)
 {
     if (w->global_config == NULL) return -1;
     if (w->global_config->illumination.include_global || w->global_config->illumination.debug_visualize_photon_map) {
@@ -1366,9 +1368,10 @@ frt_oracle_render_rows(Camera cam, World w, size_t usteps, size_t vsteps, bool j
     jb.vsteps = vsteps;
     jb.row_begin = row_begin;
     jb.row_end = row_end;
+    jb.row_stride = row_stride > 0 ? row_stride : 1;
     jb.jitter = jitter;
     jb.out = out;
-    atomic_init(&jb.next_row, row_begin);
+    atomic_init(&jb.next_row, 0);
     pthread_mutex_init(&jb.stats_lock, NULL);
     if (nthreads < 1) nthreads = 1;
     if (nthreads == 1) {
@@ -1382,4 +1385,13 @@ frt_oracle_render_rows(Camera cam, World w, size_t usteps, size_t vsteps, bool j
     pthread_mutex_destroy(&jb.stats_lock);
     if (stats) *stats = jb.stats;
     return 0;
+}
+
+/* rows row_begin, row_begin + 1, ... (out: one row after another) */
+int
+frt_oracle_render_rows(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter,
+                       size_t row_begin, size_t row_end, int nthreads, double *out, frt_oracle_stats *stats)
+{
+    return frt_oracle_render_rows_strided(cam, w, usteps, vsteps, jitter, row_begin, row_end, 1, nthreads, out,
+                                          stats);
 }

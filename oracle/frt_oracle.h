@@ -40,6 +40,10 @@ typedef struct frt_oracle_stats {
 int frt_oracle_render_rows(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter,
                            size_t row_begin, size_t row_end, int nthreads, double *out,
                            frt_oracle_stats *stats);
+/* rows row_begin, row_begin + row_stride, ... below row_end (one row job each; out: one row after another) */
+int frt_oracle_render_rows_strided(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter,
+                                   size_t row_begin, size_t row_end, size_t row_stride, int nthreads, double *out,
+                                   frt_oracle_stats *stats);
 
 #ifdef __cplusplus
 }

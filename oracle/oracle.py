@@ -37,27 +37,30 @@ def oracle_lib() -> ctypes.CDLL:
             build.build_oracle()
         lib = ctypes.CDLL(build.ORACLE_LIB)
         vp = ctypes.c_void_p
-        lib.frt_oracle_render_rows.restype = ctypes.c_int
-        lib.frt_oracle_render_rows.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool,
-                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, vp,
-                                               ctypes.POINTER(OracleStats)]
+        lib.frt_oracle_render_rows_strided.restype = ctypes.c_int
+        lib.frt_oracle_render_rows_strided.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool,
+                                                       ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                                       vp, ctypes.POINTER(OracleStats)]
         _lib = lib
     return _lib
 
 
-def render(scene, row_begin: int = 0, row_end: int | None = None, threads: int = 0, stats: bool = False):
-    """Render rows [row_begin, row_end) of a captured scene on the CPU; (rows, width, 4) float64."""
+def render(scene, row_begin: int = 0, row_end: int | None = None, threads: int = 0, stats: bool = False,
+           row_stride: int = 1):
+    """Render rows row_begin, row_begin + row_stride, ... below row_end of a captured scene on the CPU;
+    (rows, width, 4) float64."""
     lib = oracle_lib()
     row_end = scene.height if row_end is None else row_end
-    out = np.zeros((row_end - row_begin, scene.width, 4), dtype=np.float64)
+    nrows = len(range(row_begin, row_end, row_stride))
+    out = np.zeros((nrows, scene.width, 4), dtype=np.float64)
     st = OracleStats()
     threads = threads or min(8, os.cpu_count() or 1)
     # drand48 (pixel jitter, aperture samples) continues from the state the scene's main() left,
     # as in the reference's executable; with one thread the draw order is the reference's
     host_lib().frt_set_drand48((ctypes.c_ushort * 3)(*scene.drand48_state))
-    rc = lib.frt_oracle_render_rows(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter,
-                                    row_begin, row_end, threads, out.ctypes.data_as(ctypes.c_void_p),
-                                    ctypes.byref(st))
+    rc = lib.frt_oracle_render_rows_strided(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter,
+                                            row_begin, row_end, row_stride, threads,
+                                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
     if rc != 0:
         raise RuntimeError("oracle render failed (rc=%d)" % rc)
     if stats:

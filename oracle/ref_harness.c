@@ -120,6 +120,11 @@ frt_ref_render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jit
      * (pixel jitter, aperture samples) after the scene is built; after a photon
      * pass with a salted seed, so the render does not replay the photon stream */
     reseed_from_env(g_traced_photons ? 0x5bd1e995ULL : 0);
+    /* FRT_REF_THREADS: the pool size of the reference's render_multi (renderer.c:244-281 sizes its pthread
+     * pool by threading.num_threads), e.g. the CPU share of the machine it is timed on */
+    const char *thr = getenv("FRT_REF_THREADS");
+    if (thr != NULL && atoi(thr) > 0)
+        w->global_config->threading.num_threads = (size_t)atoi(thr);
     struct timespec a, b;
     clock_gettime(CLOCK_MONOTONIC, &a);
     Canvas c = render_multi(cam, w, usteps, vsteps, jitter);

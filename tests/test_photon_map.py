@@ -19,7 +19,6 @@ reference's pm_irradiance_estimate results (irradiance and photons used, pm.c:91
   another order).
 """
 import ctypes
-import math
 import os
 
 import numpy as np
@@ -45,15 +44,13 @@ def maps_of(fx):
 
 
 def stored_order(fx, m):
-    """The map's photons in storage order (before pm_balance), as the device receives them."""
+    """The map's photons in storage order (before pm_balance), as the device receives them: positions,
+    powers and the stored direction bytes (theta, phi)."""
     kd = fx["kd_%d" % m]
     order = np.argsort(fx["perm_%d" % m])
     st = kd[order]
     pos, power = np.ascontiguousarray(st[:, 0:3]), np.ascontiguousarray(st[:, 3:6])
-    a = st[:, 6] * (1.0 / 256.0) * math.pi  # pm_photon_dir (pm.c:80-86)
-    b = st[:, 7] * (1.0 / 256.0) * math.pi
-    d = np.stack([np.sin(a) * np.cos(2.0 * b), np.sin(a) * np.sin(2.0 * b), np.cos(a)], axis=1)
-    return pos, power, np.ascontiguousarray(d)
+    return pos, power, np.ascontiguousarray(st[:, 6:8].astype(np.uint8))
 
 
 def heap_kd(fx, m):
@@ -161,12 +158,12 @@ def test_device_estimates_match_reference(built, fx):
     radius, k, cone_k = float(fx["params"][0]), int(fx["params"][1]), float(fx["params"][2])
     bad = []
     for m in maps_of(fx):
-        pos, power, d = stored_order(fx, m)
+        pos, power, tpb = stored_order(fx, m)
         idx = np.nonzero(fx["query_map"] == m)[0]
         q = np.ascontiguousarray(np.concatenate([fx["query_pos"][idx], fx["query_normal"][idx]], axis=1))
         irrad = np.zeros((len(idx), 3))
         found = np.zeros(len(idx), np.int64)
-        rc = lib.frt_pm_estimate(0, pos.ctypes.data, power.ctypes.data, d.ctypes.data, len(pos), q.ctypes.data,
+        rc = lib.frt_pm_estimate(0, pos.ctypes.data, power.ctypes.data, tpb.ctypes.data, len(pos), q.ctypes.data,
                                  len(idx), radius, k, cone_k, irrad.ctypes.data, found.ctypes.data)
         assert rc == 0, lib.frt_last_error()
         assert np.array_equal(found, fx["found"][idx]), (m, np.nonzero(found != fx["found"][idx])[0][:10])
@@ -185,15 +182,16 @@ def test_device_estimate_edge_cases(built):
                                     ctypes.c_int32, ctypes.c_double, vp, vp]
     import pm_oracle
 
-    def run(pos, power, d, q, radius, k, cone_k):
+    def run(pos, power, tp, q, radius, k, cone_k):
         irrad = np.zeros((len(q), 3))
         found = np.zeros(len(q), np.int64)
-        pos, power, d, q = (np.ascontiguousarray(a, dtype=np.float64) for a in (pos, power, d, q))
-        assert lib.frt_pm_estimate(0, pos.ctypes.data, power.ctypes.data, d.ctypes.data, len(pos), q.ctypes.data,
+        pos, power, q = (np.ascontiguousarray(a, dtype=np.float64) for a in (pos, power, q))
+        tpb = np.ascontiguousarray(tp, dtype=np.uint8)
+        assert lib.frt_pm_estimate(0, pos.ctypes.data, power.ctypes.data, tpb.ctypes.data, len(pos), q.ctypes.data,
                                    len(q), radius, k, cone_k, irrad.ctypes.data, found.ctypes.data) == 0
         return irrad, found
 
-    def oracle(pos, power, d, q, radius, k, cone_k):
+    def oracle(pos, power, tp, q, radius, k, cone_k):
         n = len(pos)
         pbal, plane = pm_oracle.balance(np.concatenate([np.zeros((1, 3)), pos]))
         kd = np.zeros((n + 1, 9))
@@ -213,17 +211,26 @@ def test_device_estimate_edge_cases(built):
     # many equal photons at one point: binary64 ties (which of them the search keeps is not reproduced;
     # equal records make the estimate independent of it)
     pos[:400], power[:400], tp[:400] = 0.25, 5e-4, (17.0, 101.0)
-    a, b = tp[:, 0] * math.pi / 256.0, tp[:, 1] * math.pi / 256.0
-    d = np.stack([np.sin(a) * np.cos(2 * b), np.sin(a) * np.sin(2 * b), np.cos(a)], axis=1)
     q = np.concatenate([rng.uniform(-1.0, 1.0, (40, 3)), rng.normal(size=(40, 3))], axis=1)
     q[:, 3:] /= np.linalg.norm(q[:, 3:], axis=1, keepdims=True)
     q[0, 0:3] = (0.26, 0.25, 0.24)  # at the ties
     q[-1, 0:3] = 40.0  # nothing in range
     for radius, k in ((0.2, 30), (0.5, 5000)):
-        irr_d, f_d = run(pos, power, d, q, radius, k, 1.1)
-        irr_o, f_o = oracle(pos, power, d, q, radius, k, 1.1)
+        irr_d, f_d = run(pos, power, tp, q, radius, k, 1.1)
+        irr_o, f_o = oracle(pos, power, tp, q, radius, k, 1.1)
         assert np.array_equal(f_d, f_o)
         assert _close(irr_d, irr_o, DEVICE_RTOL).all()
+    # a larger map of distinct powers (70 000 photons)
+    m2 = 70000
+    pos2 = rng.uniform(-1.0, 1.0, (m2, 3))
+    power2 = rng.uniform(0.0, 1e-3, (m2, 3))
+    tp2 = rng.integers(0, 256, (m2, 2)).astype(np.float64)
+    q2 = q[:6].copy()
+    q2[:, 0:3] = pos2[:6] + 0.01
+    irr_d, f_d = run(pos2, power2, tp2, q2, 0.2, 40, 1.1)
+    irr_o, f_o = oracle(pos2, power2, tp2, q2, 0.2, 40, 1.1)
+    assert np.array_equal(f_d, f_o) and (f_d == 40).all()
+    assert _close(irr_d, irr_o, DEVICE_RTOL).all()
     # no photons: nothing found, a zero estimate
-    irr_d, f_d = run(np.zeros((0, 3)), np.zeros((0, 3)), np.zeros((0, 3)), q[:4], 0.2, 30, 1.1)
+    irr_d, f_d = run(np.zeros((0, 3)), np.zeros((0, 3)), np.zeros((0, 2)), q[:4], 0.2, 30, 1.1)
     assert (f_d == 0).all() and (irr_d == 0).all()
