@@ -194,26 +194,52 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
 
 
 def gather_roofline(gd: dict) -> dict:
-    """k_gather_est (the GI frame's dominant kernel): the photon-map estimate per final-gather ray. Its
-    bytes depend on the photons within reach of each query, so no algorithmic byte model is claimed:
-    `achieved` is the HBM-side traffic per query measured by PMC (FETCH_SIZE + WRITE_SIZE, committed
-    profile of the same scene at 480x270) times this frame's queries per launch, over the live
-    event-timed launch duration. The SQ counters of that profile put ~59 % of wave cycles in memory waits."""
+    """k_gather_est (the GI frame's dominant kernel): the photon-map estimate per final-gather ray.
+    Algorithmic bytes per query (profiles/r03_gi_estimate_counters.json: device counters of the estimate,
+    tools/prof_gi_full.sh): the binary32 positions of the candidates it scans (16 B each), the 80-byte
+    records of the photons it uses, its 96-byte request and 24-byte result. `achieved` = that per query x
+    this frame's queries per launch over the live event-timed launch duration; `traffic` = the PMC
+    FETCH_SIZE (x2, the guide's gfx950 correction for wide coalesced reads) + WRITE_SIZE per launch of
+    the same workload (profiles/r03_pmc_k_gather_est_cornell_gi_1920x1080_8x8.json)."""
     n = gd["sub_launches"]["k_gather_est"]
     avg_ms = gd["sub_ms"]["k_gather_est"] / n
-    found = latest_pmc("k_gather_est", "cornell_gi_480x270_8x8")
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
             "kernel": "k_gather_est", "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": n}
-    if found:
-        path, t = found
-        q = t["SQ_WAVES_per_launch"] * 64.0
-        per_query = (t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)) / q
+    model = os.path.join(ROOT, "profiles", "r03_gi_estimate_counters.json")
+    if os.path.exists(model):
+        m = json.load(open(model))
+        per_query = m["algorithmic_bytes_per_query"]
         per_launch = per_query * gd["gather_rays"] / n
         ach = per_launch / (avg_ms * 1e-3) / 1e9
-        roof.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": round(per_launch),
-                     "traffic_bytes_per_query": round(per_query, 1), "traffic_source": os.path.relpath(path, ROOT),
+        roof.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_per_query": round(per_query, 1),
+                     "algorithmic_bytes_per_launch": round(per_launch),
+                     "candidates_per_query": round(m["candidates_read_per_query"], 1),
+                     "records_per_query": round(m["records_read_per_query"], 1),
+                     "model_source": os.path.relpath(model, ROOT)})
+    found = latest_pmc("k_gather_est", GI_SCENE)
+    if found:
+        path, t = found
+        traffic = 2.0 * t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)
+        roof.update({"traffic": round(traffic), "traffic_source": os.path.relpath(path, ROOT),
+                     "rocprof_avg_launch_ms": round(t.get("rocprof_avg_ms", 0.0), 4),
+                     "valu_insts_per_query": round(t["SQ_INSTS_VALU_per_launch"] / (64.0 * t["SQ_WAVES_per_launch"]), 1),
+                     "salu_insts_per_query": round(t["SQ_INSTS_SALU_per_launch"] / (64.0 * t["SQ_WAVES_per_launch"]), 1),
                      "wait_any_frac": round(t.get("sq_wait_any_frac_of_wave_cycles", 0.0), 3)})
     return roof
+
+
+def heartbeat(period_s: float = 60.0) -> None:
+    """A progress line on stderr every minute while the bench runs (long profiled runs print nothing else)."""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period_s)
+            log("bench: running, %.0f s" % (time.time() - t0))
+
+    threading.Thread(target=beat, daemon=True).start()
 
 
 def main():
@@ -228,6 +254,7 @@ def main():
     ap.add_argument("--no-render-multi", action="store_true", help="skip the drop-in entry point timing")
     args = ap.parse_args()
     launch_ranks_if_needed(args)
+    heartbeat()
 
     import torch
     import torch.distributed as dist

@@ -606,13 +606,28 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         irrad[2] *= tmp;
     };
     if (total <= (unsigned)k) {  // every photon in range: no heap, dist2[0] = max_dist^2
-        visit([&](int32_t p, bool in, unsigned) {
-            EST_LANES(15, in);
-            if (in) {
-                const PhotonRec pr = photon_rec(M, p);
-                accumulate(pr, p, sqrt_w(pr.d2(x)));
+        if (listed) {  // two chunks of the list per round trip
+            for (unsigned base = 0; base < count; base += 128) {
+                const unsigned i0 = base + (unsigned)lane, i1 = i0 + 64u;
+                const bool a = i0 < count, b = i1 < count;
+                const int32_t pa = a ? (int32_t)L.ent[i0].y : 0, pb = b ? (int32_t)L.ent[i1].y : 0;
+                EST_LANES(15, a);
+                EST_LANES(15, b);
+                PhotonRec ra, rb;
+                if (a) ra = photon_rec(M, pa);
+                if (b) rb = photon_rec(M, pb);
+                if (a) accumulate(ra, pa, sqrt_w(ra.d2(x)));
+                if (b) accumulate(rb, pb, sqrt_w(rb.d2(x)));
             }
-        });
+        } else {
+            visit([&](int32_t p, bool in, unsigned) {
+                EST_LANES(15, in);
+                if (in) {
+                    const PhotonRec pr = photon_rec(M, p);
+                    accumulate(pr, p, sqrt_w(pr.d2(x)));
+                }
+            });
+        }
         finish(r2);
         EST_STAMP(2);
         return found;

@@ -21,6 +21,8 @@ with four GPU renders (seeds) against the K references:
 * RMSE: the same ratio <= 1.6 (tail guard);
 * image-mean bias within 4 standard errors from the references' spread.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -79,3 +81,32 @@ def test_gpu_stochastic_seeding(built, name):
     even, odd = r.render(0, None, 2, seed=1), r.render(1, None, 2, seed=1)
     assert np.array_equal(a[0::2], even) and np.array_equal(a[1::2], odd)
     r.close()
+
+
+@pytest.mark.gpu
+def test_gpu_gi_full_size_row_bands(built):
+    """cfg5 at full size (BASELINE configs[4]: the shipped cornell GI configuration at 1920x1080, 8x8 CMJ,
+    1M photons, k = 200): two 60-row bands at one seed. Properties: finite; bit-identical on repeat and
+    under the 2-way row interleave of a multi-GPU split; and each band's mean within the spread of the
+    reference's own renders of the same view. The 1920x1080 camera keeps the 64x64 golden's horizontal
+    extent (camera.c: half_width = tan(fov / 2) for aspect >= 1), so 1920-row r lies on 64-row
+    14 + r / 30 and a 60-row band starting at a multiple of 30 covers exactly two rows of cornell_gi_64
+    (six independent reference renders, each with its own photon maps)."""
+    from fast_ray_tracer_amd.runtime import GpuRenderer
+    r = GpuRenderer(load_scene("cornell_gi_1920x1080_8x8"))
+    refs = np.load(os.path.join(os.path.dirname(__file__), "golden", "cornell_gi_64.npz"))["refs"]
+    try:
+        for r0 in (240, 600):
+            band = r.render(r0, r0 + 60, seed=0x5EED)
+            assert band.shape == (60, 1920, 4) and np.isfinite(band).all()
+            assert np.array_equal(band, r.render(r0, r0 + 60, seed=0x5EED))
+            assert np.array_equal(band[0::2], r.render(r0, r0 + 60, 2, seed=0x5EED))
+            assert np.array_equal(band[1::2], r.render(r0 + 1, r0 + 60, 2, seed=0x5EED))
+            s0 = 14 + r0 // 30
+            ref_means = refs[:, s0:s0 + 2].mean(axis=(1, 2))  # (6, 3)
+            mu, sd = ref_means.mean(axis=0), ref_means.std(axis=0, ddof=1)
+            got = band[:, :, :3].mean(axis=(0, 1))
+            print(f"band {r0}: gpu {got} reference {mu} +- {sd}")
+            assert (np.abs(got - mu) <= 4.0 * sd + 0.01 * mu).all(), (r0, got, mu, sd)
+    finally:
+        r.close()
