@@ -63,6 +63,109 @@ struct NodeRec {
 };
 static_assert(sizeof(NodeRec) == 216, "NodeRec layout");
 
+// NodeRec in HBM: the fields every path node needs (14 column words) and its material colours (13
+// words), which k_prepare stores only for materials with patterns on them (kOwnColors; every other
+// reader takes them from the material table): the colours of pattern-free materials are never written
+// or read per node, and a missed ray writes only its material / parent / slot words.
+struct NodeCore {
+    double over_point[3];
+    uint64_t key;
+    int32_t material, parent, slot, flags;
+    double normalv[3], eyev[3];
+    double over_d, rf;
+};
+struct NodeColors {
+    double Ka[3], Kd[3], Ks[3], refl[3];
+    double Ns;
+};
+static_assert(sizeof(NodeCore) == 112 && sizeof(NodeColors) == 104, "NodeCols layout");
+enum : int32_t { kOwnColors = 64 };  // (NodeFlags bit) the node's colours are in NodeCols::col
+
+struct NodeCols {
+    Cols<NodeCore> core;
+    Cols<NodeColors> col;
+    static size_t bytes(int64_t cap) { return Cols<NodeCore>::bytes(cap) + Cols<NodeColors>::bytes(cap); }
+    void set(uint64_t* base, int64_t cap) {  // (host) one allocation of bytes(cap)
+        core.w = base;
+        core.cap = cap;
+        col.w = base + (size_t)Cols<NodeCore>::kWords * cap;
+        col.cap = cap;
+    }
+    __device__ __forceinline__ void store(int64_t i, const NodeRec& v, bool own_colors) const {
+        NodeCore c;
+        for (int k = 0; k < 3; ++k) {
+            c.over_point[k] = v.over_point[k];
+            c.normalv[k] = v.normalv[k];
+            c.eyev[k] = v.eyev[k];
+        }
+        c.key = v.key;
+        c.material = v.material;
+        c.parent = v.parent;
+        c.slot = v.slot;
+        c.flags = v.flags | (own_colors ? kOwnColors : 0);
+        c.over_d = v.over_d;
+        c.rf = v.rf;
+        core.store(i, c);
+        if (own_colors) {
+            NodeColors o;
+            for (int k = 0; k < 3; ++k) {
+                o.Ka[k] = v.Ka[k];
+                o.Kd[k] = v.Kd[k];
+                o.Ks[k] = v.Ks[k];
+                o.refl[k] = v.refl[k];
+            }
+            o.Ns = v.Ns;
+            col.store(i, o);
+        }
+    }
+    // a missed ray: material -1 with its parent and slot (the words k_combine reads)
+    __device__ __forceinline__ void store_miss(int64_t i, int32_t parent, int32_t slot) const {
+        const uint64_t w4 = (uint64_t)(uint32_t)-1 | ((uint64_t)(uint32_t)parent << 32);
+        const uint64_t w5 = (uint64_t)(uint32_t)slot;
+        core.w[4 * core.cap + i] = w4;
+        core.w[5 * core.cap + i] = w5;
+    }
+    __device__ __forceinline__ NodeRec load(int64_t i, const frt_material* __restrict__ mats) const {
+        const NodeCore c = core.load(i);
+        NodeRec v;
+        for (int k = 0; k < 3; ++k) {
+            v.over_point[k] = c.over_point[k];
+            v.normalv[k] = c.normalv[k];
+            v.eyev[k] = c.eyev[k];
+        }
+        v.key = c.key;
+        v.material = c.material;
+        v.parent = c.parent;
+        v.slot = c.slot;
+        v.flags = c.flags;
+        v.over_d = c.over_d;
+        v.rf = c.rf;
+        if (c.material < 0) {
+            for (int k = 0; k < 3; ++k) v.Ka[k] = v.Kd[k] = v.Ks[k] = v.refl[k] = 0.0;
+            v.Ns = 0.0;
+        } else if (c.flags & kOwnColors) {
+            const NodeColors o = col.load(i);
+            for (int k = 0; k < 3; ++k) {
+                v.Ka[k] = o.Ka[k];
+                v.Kd[k] = o.Kd[k];
+                v.Ks[k] = o.Ks[k];
+                v.refl[k] = o.refl[k];
+            }
+            v.Ns = o.Ns;
+        } else {
+            const frt_material& M = mats[c.material];
+            for (int k = 0; k < 3; ++k) {
+                v.Ka[k] = M.Ka[k];
+                v.Kd[k] = M.Kd[k];
+                v.Ks[k] = M.Ks[k];
+                v.refl[k] = M.refl[k];
+            }
+            v.Ns = M.Ns;
+        }
+        return v;
+    }
+};
+
 
 struct QueuedRay {
     double o[3];
@@ -240,7 +343,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
 // prepare_computations + spawn of the reflection / refraction rays (renderer.c:369-605)
 template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
-                                                    const HitRec* __restrict__ hits, Cols<NodeRec> rec,
+                                                    const HitRec* __restrict__ hits, NodeCols rec,
                                                     ShadowHead* __restrict__ heads,
                                                     QueuedRay* __restrict__ next_q,
                                                     unsigned long long* counters, unsigned* err) {
@@ -280,11 +383,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
     const HitRec hr = hits[node];
     PSTAMP(1);
     if (hr.node < 0) {
-        NodeRec miss{};
-        miss.material = -1;
-        miss.parent = parent;
-        miss.slot = slot;
-        rec.store(node, miss);
+        rec.store_miss(node, parent, slot);
         heads[node].material = -1;
         return;
     }
@@ -387,7 +486,9 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
     }
     nr.flags = flags;
     PSTAMP(3);
-    rec.store(node, nr);
+    // the colours per node only where a pattern makes them vary (prepare: map_Ka / Kd / Ks / refl / Ns)
+    const bool own = kPat && (M.map_Ka >= 0 || M.map_Kd >= 0 || M.map_Ks >= 0 || M.map_refl >= 0 || M.map_Ns >= 0);
+    rec.store(node, nr, own);
     ShadowHead hd;
     for (int k = 0; k < 3; ++k) hd.over_point[k] = c.over_point[k];
     hd.key = key;
@@ -551,7 +652,7 @@ __device__ __forceinline__ bool shade_heavy(const DevScene& S, const int32_t* __
 // listed nodes with every lane busy.
 constexpr int kShadeSegs = 64;
 static_assert(kShadeSegs == jit::kMixSegs, "k_shade_lit reads its slots with jit::mix_slot");
-__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<NodeRec> rec, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols rec, int64_t n,
                                                   const int32_t* __restrict__ counts, Cols<Tri9> surface,
                                                   uint32_t* __restrict__ lit, unsigned* __restrict__ lcount,
                                                   uint32_t segcap) {
@@ -559,7 +660,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<Node
     bool heavy = false, mine = false;
     NodeRec nr{};
     if (i < n) {
-        nr = rec.load(i);
+        nr = rec.load(i, S.materials);
         mine = nr.material >= 0;
         heavy = mine && lit != nullptr && shade_heavy(S, counts, i);
     }
@@ -586,7 +687,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, Cols<Node
 #ifndef FRT_SHADE_WAVES
 #define FRT_SHADE_WAVES 1
 #endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_SHADE_WAVES, 8))) k_shade_lit(DevScene S, Batch B, Cols<NodeRec> rec,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_SHADE_WAVES, 8))) k_shade_lit(DevScene S, Batch B, NodeCols rec,
                                                       const int32_t* __restrict__ counts, Cols<Tri9> surface,
                                                       const uint32_t* __restrict__ lit,
                                                       const unsigned* __restrict__ lcount, uint32_t segcap) {
@@ -605,7 +706,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
     if (m >= total) return;
     const int64_t i = (int64_t)lit[slot];
-    const NodeRec nr = rec.load(i);
+    const NodeRec nr = rec.load(i, S.materials);
     double out[12];
     shade_node(S, B, nr, i, counts, out);
     tri_store(surface, i, out);
@@ -613,12 +714,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
 
 // bottom-up combine of one level (shade_hit's specular block, renderer.c:773-822)
 // (level 0: samples land in sample_out in sample order, coalesced stores; k_resolve reads each pixel's run)
-__global__ void __launch_bounds__(kBlock) k_combine(Cols<NodeRec> rec, int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
+__global__ void __launch_bounds__(kBlock) k_combine(NodeCols rec, int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
                                                     Cols<Tri9> parent_child, Cols<Tri9> sample_out, int32_t spp,
                                                     const frt_material* __restrict__ mats, int32_t include_specular) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec nr = rec.load(i);
+    const NodeRec nr = rec.load(i, mats);
     double col[12];
     if (nr.material < 0) {
         for (int k = 0; k < 12; ++k) col[k] = 0.0;
@@ -949,14 +1050,14 @@ __device__ inline void wave_photon_estimates(const PhotonMapDev& M, const DevSce
 }
 
 // per shaded node: the visualisation term (lighting_gi) and the caustics term (renderer.c:740-761)
-__global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, Cols<NodeRec> rec, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, NodeCols rec, int64_t n,
                                                     double* __restrict__ gi_extra) {
     FRT_EST_LDS(lds, kEstCap);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     NodeRec nr{};
     bool want = false;
     if (i < n) {
-        nr = rec.load(i);
+        nr = rec.load(i, S.materials);
         want = nr.material >= 0 && any_positive(nr.Kd);
     }
     double vis[3] = {0, 0, 0}, cau[3] = {0, 0, 0};
@@ -985,14 +1086,14 @@ __global__ void __launch_bounds__(kBlock) k_gi_node(DevScene S, Cols<NodeRec> re
 
 // final_gather's rays (renderer.c:648-687): gu x gv cosine-weighted hemisphere
 // directions (a jittered CMJ pattern per gather) from over_point
-__global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed, Cols<NodeRec> rec,
+__global__ void __launch_bounds__(kBlock) k_gather_gen(DevScene S, uint64_t seed, NodeCols rec,
                                                        int64_t node0, int64_t nodes, QueuedRay* __restrict__ gq) {
     const int G = S.cfg.gi_usteps * S.cfg.gi_vsteps;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nodes * G) return;
     const int64_t node = node0 + t / G;
     const int slot = (int)(t % G);
-    const NodeRec nr = rec.load(node);
+    const NodeRec nr = rec.load(node, S.materials);
     QueuedRay qr;
     qr.key = nr.key;
     qr.slot = slot;
@@ -1165,14 +1266,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
 }
 
 // final_gather's sum (slot order = the reference's v-outer, u-inner loop), x 2 pi / rays, x over_Kd
-__global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, Cols<NodeRec> rec, int64_t node0,
+__global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, NodeCols rec, int64_t node0,
                                                           int64_t nodes, const double* __restrict__ gather_col,
                                                           double* __restrict__ fgather) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nodes) return;
     const int64_t node = node0 + t;
     const int G = S.cfg.gi_usteps * S.cfg.gi_vsteps;
-    const NodeRec nr = rec.load(node);
+    const NodeRec nr = rec.load(node, S.materials);
     double* out = fgather + 3 * node;
     out[0] = out[1] = out[2] = 0.0;
     if (nr.material < 0 || !any_positive(nr.Kd)) return;
@@ -1184,12 +1285,12 @@ __global__ void __launch_bounds__(kBlock) k_gather_reduce(DevScene S, Cols<NodeR
 }
 
 // shade_hit's GI block (renderer.c:727-770): ambient += indirect, final gather, caustics; clamp to sqrt(3)
-__global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, Cols<NodeRec> rec, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, NodeCols rec, int64_t n,
                                                      const double* __restrict__ gi_extra,
                                                      const double* __restrict__ fgather, Cols<Tri9> surface) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec nr = rec.load(i);
+    const NodeRec nr = rec.load(i, S.materials);
     if (nr.material < 0 || !any_positive(nr.Kd)) return;
     double a[12];
     tri_load(surface, i, a);
@@ -1249,7 +1350,7 @@ struct frt_scene_handle {
                                               // then {waves, lanes} per node (frt_jit_rt.hpp node_stat)
     // work buffers (grow on demand)
     struct Level {
-        frt::Cols<frt::NodeRec> rec;
+        frt::NodeCols rec;
         frt::ShadowHead* head = nullptr;
         frt::QueuedRay* q = nullptr;
         frt::Cols<frt::Tri9> surface;
@@ -1820,7 +1921,7 @@ void frt_scene_release(frt_scene_handle* h) {
     }
     for (void* p : h->owned) hip_ignore(hipFree(p));
     for (auto& L : h->levels) {
-        hip_ignore(hipFree(L.rec.w));
+        hip_ignore(hipFree(L.rec.core.w));
         hip_ignore(hipFree(L.head));
         hip_ignore(hipFree(L.q));
         hip_ignore(hipFree(L.surface.w));
@@ -1862,7 +1963,7 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     auto& L = h->levels[d];
     if (need <= L.cap) return 0;
     int64_t nc = std::max<int64_t>(need, L.cap * 2);
-    hip_ignore(hipFree(L.rec.w));
+    hip_ignore(hipFree(L.rec.core.w));
     hip_ignore(hipFree(L.head));
     L.head = nullptr;
     hip_ignore(hipFree(L.q));
@@ -1874,8 +1975,11 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     L.surface = {};
     L.child = {};
     L.counts = nullptr;
-    FRT_HIP(hipMalloc((void**)&L.rec.w, frt::Cols<frt::NodeRec>::bytes(nc)));
-    L.rec.cap = nc;
+    {
+        void* p = nullptr;
+        FRT_HIP(hipMalloc(&p, frt::NodeCols::bytes(nc)));
+        L.rec.set((uint64_t*)p, nc);
+    }
     FRT_HIP(hipMalloc((void**)&L.head, nc * sizeof(frt::ShadowHead)));
     FRT_HIP(hipMalloc((void**)&L.q, nc * sizeof(frt::QueuedRay)));
     FRT_HIP(hipMalloc((void**)&L.surface.w, frt::Cols<frt::Tri9>::bytes(nc)));
