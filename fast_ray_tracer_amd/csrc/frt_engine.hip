@@ -493,7 +493,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const Q
     for (int k = 0; k < 3; ++k) hd.over_point[k] = c.over_point[k];
     hd.key = key;
     hd.material = c.material;
-    for (int k = 0; k < 5; ++k) hd.pad[k] = 0;
+    hd.pad = 0;
     heads[node] = hd;
     PSTAMP(4);
 }
@@ -2924,11 +2924,12 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->hits = hits;
         st->shadow_rays = h->S.cfg.include_direct ? hits * (uint64_t)h->samples_per_node : 0;
         // DESIGN.md byte model of the per-ray shadow kernel: per walked (node, light part) pair its 4-byte list
-        // entry and the node's 64-byte ShadowHead read, one 4-byte count written; the generic walk: per shaded
-        // node the ShadowHead + one 4-byte count per light
+        // entry and 4-byte resume word and the node's ShadowHead read, one 4-byte count written; the generic
+        // walk: per shaded node the ShadowHead + one 4-byte count per light
+        constexpr double kHead = (double)sizeof(frt::ShadowHead);
         st->shadow_kernel_bytes = !(h->S.cfg.include_direct && h->samples_per_node > 0) ? 0.0
-                                  : h->jit_shadow != nullptr ? (double)h->pairs_walked * (4.0 + 64.0 + 4.0)
-                                                             : (double)hits * (64.0 + 4.0 * h->S.num_lights);
+                                  : h->jit_shadow != nullptr ? (double)h->pairs_walked * (4.0 + 4.0 + kHead + 4.0)
+                                                             : (double)hits * (kHead + 4.0 * h->S.num_lights);
         st->errors = err;
         st->shadow_jit = h->jit_shadow != nullptr ? 1 : 0;
         st->shadow_rays_walked = h->jit_shadow != nullptr ? h->rays_walked : st->shadow_rays;

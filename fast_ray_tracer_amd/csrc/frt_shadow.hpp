@@ -64,16 +64,16 @@ __device__ __forceinline__ int64_t queue_slot(const Batch& B, int64_t i) {
     return (int64_t)lo * B.qsegcap + (i - B.qprefix[lo]);
 }
 
-// what k_shadow reads of a path node, one 64-byte line per node (the shadow
-// pass re-reads it from 100 lanes; keeping it apart from the 216-byte NodeRec
-// keeps the pass's HBM traffic at one line per node)
-struct alignas(64) ShadowHead {
+// what the shadow pass reads of a path node, 40 bytes per node (the pass re-reads it from 100 lanes;
+// keeping it apart from the path-node columns keeps its HBM traffic at about one line per node, and the
+// unpadded record keeps k_prepare's writes of it at 40 bytes: a wave stores 20 whole lines)
+struct alignas(8) ShadowHead {
     double over_point[3];
     uint64_t key;
     int32_t material;  // -1: the ray missed
-    int32_t pad[5];
+    int32_t pad;
 };
-static_assert(sizeof(ShadowHead) == 64, "ShadowHead layout");
+static_assert(sizeof(ShadowHead) == 40, "ShadowHead layout");
 
 // one lane per (path node, light sample j); lanes of a node are consecutive
 struct ShadowLane {
