@@ -1456,6 +1456,240 @@ int frt_device_count(void) {
     return n;
 }
 
+// ---- meshes (frt_traverse.hpp MeshDesc): group subtrees of groups and triangles only ----
+// A mesh root: a group whose children are all groups without transforms or triangles without transforms,
+// recursively (the group itself may carry a transform: the walk applies it before the search), outside
+// any CSG, with at least kMeshMinTris triangles, and not inside a larger one. Scenes the scene-specialised
+// shadow kernel takes (<= 512 nodes) keep the plain walk.
+constexpr int kMeshMinTris = 64;
+
+struct MeshBuild {
+    struct Tri {
+        double lo[3], hi[3], c[3];
+        int32_t node, prim;
+    };
+    std::vector<Tri> tris;
+    std::vector<frt::MeshNode> nodes;
+    std::vector<int2> refs;
+    int depth = 0;
+
+    static float down(double v) {
+        float f = (float)v;
+        if ((double)f > v) f = std::nextafter(f, -INFINITY);
+        return f;
+    }
+    static float up(double v) {
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, INFINITY);
+        return f;
+    }
+    struct Sub {
+        double lo[3], hi[3];
+        int32_t ref, mindfs;
+    };
+    // binned SAH over tris[b, e); returns the subtree's box, reference and smallest pre-order index
+    Sub build(int b, int e, int d) {
+        depth = std::max(depth, d);
+        Sub out;
+        for (int a = 0; a < 3; ++a) {
+            out.lo[a] = INFINITY;
+            out.hi[a] = -INFINITY;
+        }
+        out.mindfs = 0x7fffffff;
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) {
+                out.lo[a] = std::min(out.lo[a], tris[(size_t)i].lo[a]);
+                out.hi[a] = std::max(out.hi[a], tris[(size_t)i].hi[a]);
+                clo[a] = std::min(clo[a], tris[(size_t)i].c[a]);
+                chi[a] = std::max(chi[a], tris[(size_t)i].c[a]);
+            }
+        for (int i = b; i < e; ++i) out.mindfs = std::min(out.mindfs, tris[(size_t)i].node);
+        const int n = e - b;
+        if (n <= 4) {  // leaf: triangles in pre-order
+            std::sort(tris.begin() + b, tris.begin() + e, [](const Tri& x, const Tri& y) { return x.node < y.node; });
+            const int first = (int)refs.size();
+            for (int i = b; i < e; ++i) refs.push_back(make_int2(tris[(size_t)i].node, tris[(size_t)i].prim));
+            out.ref = ~((first << 3) | (n - 1));
+            return out;
+        }
+        constexpr int kBins = 16;
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+        int mid = b + n / 2;
+        const double ext = chi[axis] - clo[axis];
+        if (ext > 0.0) {
+            struct Bin {
+                double lo[3], hi[3];
+                int n = 0;
+            } bins[kBins];
+            for (auto& bn : bins)
+                for (int a = 0; a < 3; ++a) {
+                    bn.lo[a] = INFINITY;
+                    bn.hi[a] = -INFINITY;
+                }
+            auto bin_of = [&](const Tri& t) {
+                return std::min(kBins - 1, (int)((t.c[axis] - clo[axis]) / ext * kBins));
+            };
+            for (int i = b; i < e; ++i) {
+                Bin& bn = bins[bin_of(tris[(size_t)i])];
+                bn.n++;
+                for (int a = 0; a < 3; ++a) {
+                    bn.lo[a] = std::min(bn.lo[a], tris[(size_t)i].lo[a]);
+                    bn.hi[a] = std::max(bn.hi[a], tris[(size_t)i].hi[a]);
+                }
+            }
+            auto area = [](const double* lo, const double* hi) {
+                const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+                return x < 0 ? 0.0 : 2.0 * (x * y + y * z + z * x);
+            };
+            double best = INFINITY;
+            int split = -1;
+            for (int k = 1; k < kBins; ++k) {
+                double l0[3] = {INFINITY, INFINITY, INFINITY}, h0[3] = {-INFINITY, -INFINITY, -INFINITY};
+                double l1[3] = {INFINITY, INFINITY, INFINITY}, h1[3] = {-INFINITY, -INFINITY, -INFINITY};
+                int n0 = 0, n1 = 0;
+                for (int j = 0; j < kBins; ++j) {
+                    double* lo = j < k ? l0 : l1;
+                    double* hi = j < k ? h0 : h1;
+                    (j < k ? n0 : n1) += bins[j].n;
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = std::min(lo[a], bins[j].lo[a]);
+                        hi[a] = std::max(hi[a], bins[j].hi[a]);
+                    }
+                }
+                if (n0 == 0 || n1 == 0) continue;
+                const double cost = area(l0, h0) * n0 + area(l1, h1) * n1;
+                if (cost < best) {
+                    best = cost;
+                    split = k;
+                }
+            }
+            if (split > 0) {
+                auto it = std::partition(tris.begin() + b, tris.begin() + e,
+                                         [&](const Tri& t) { return bin_of(t) < split; });
+                mid = (int)(it - tris.begin());
+            }
+        }
+        if (mid <= b || mid >= e) {  // (degenerate centroids) halves in pre-order
+            std::sort(tris.begin() + b, tris.begin() + e, [](const Tri& x, const Tri& y) { return x.node < y.node; });
+            mid = b + n / 2;
+        }
+        const int self = (int)nodes.size();
+        nodes.emplace_back();
+        const Sub l = build(b, mid, d + 1), r = build(mid, e, d + 1);
+        frt::MeshNode& N = nodes[(size_t)self];
+        const Sub* c[2] = {&l, &r};
+        for (int k = 0; k < 2; ++k) {
+            for (int a = 0; a < 3; ++a) {
+                N.b[6 * k + a] = down(c[k]->lo[a]);
+                N.b[6 * k + 3 + a] = up(c[k]->hi[a]);
+            }
+            N.child[k] = c[k]->ref;
+            N.mindfs[k] = c[k]->mindfs;
+        }
+        out.ref = self;
+        return out;
+    }
+};
+
+// the scene's meshes: marks each root in wn (op = mesh index + 1), builds their BVHs (one host thread per
+// mesh), uploads them; S.meshes / num_meshes / mesh_stack
+static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<frt::WalkNode>& wn) {
+    const int nn = sc->num_nodes;
+    frt::DevScene& S = h->S;
+    S.meshes = nullptr;
+    S.num_meshes = 0;
+    S.mesh_stack = 0;
+    const char* env = std::getenv("FRT_MESH");  // FRT_MESH=0: the plain walk everywhere (A/B runs)
+    if (nn <= 512 || (env && std::strcmp(env, "0") == 0)) return 0;
+    auto is_tri = [&](int i) { return sc->nodes[i].type == FRT_TRIANGLE || sc->nodes[i].type == FRT_SMOOTH_TRIANGLE; };
+    // inner[i]: node i may sit inside a mesh (a triangle or a group without transform of such nodes)
+    std::vector<char> inner((size_t)nn, 0), in_csg((size_t)nn, 0);
+    std::vector<int> ntri((size_t)nn, 0);
+    for (int i = 0; i < nn; ++i) {
+        const int par = sc->nodes[i].parent;
+        in_csg[(size_t)i] = par >= 0 && (in_csg[(size_t)par] || sc->nodes[par].type == FRT_CSG);
+    }
+    auto children_inner = [&](int i) {
+        for (int j = i + 1; j < sc->nodes[i].skip; j = sc->nodes[j].skip)
+            if (!inner[(size_t)j]) return false;
+        return true;
+    };
+    for (int i = nn - 1; i >= 0; --i) {
+        const frt_node& nd = sc->nodes[i];
+        if (is_tri(i)) {
+            inner[(size_t)i] = nd.xform < 0;
+            ntri[(size_t)i] = 1;
+        } else if (nd.type == FRT_GROUP) {
+            for (int j = i + 1; j < nd.skip; j = sc->nodes[j].skip) ntri[(size_t)i] += ntri[(size_t)j];
+            inner[(size_t)i] = nd.xform < 0 && nd.skip > i + 1 && children_inner(i);
+        }
+    }
+    std::vector<int> roots;
+    for (int i = 0; i < nn; ++i) {
+        const frt_node& nd = sc->nodes[i];
+        if (nd.type != FRT_GROUP || in_csg[(size_t)i] || nd.skip <= i + 1 || !children_inner(i) ||
+            ntri[(size_t)i] < kMeshMinTris)
+            continue;
+        const int par = nd.parent;
+        if (par >= 0 && inner[(size_t)i] && sc->nodes[par].type == FRT_GROUP && children_inner(par) &&
+            !in_csg[(size_t)par])
+            continue;  // inside a larger mesh
+        roots.push_back(i);
+    }
+    // (a root inside another root cannot happen: a root's ancestors are not all inner)
+    std::vector<MeshBuild> mb(roots.size());
+    {
+        std::vector<std::thread> pool;
+        for (size_t m = 0; m < roots.size(); ++m)
+            pool.emplace_back([&, m]() {
+                const int g = roots[m];
+                MeshBuild& B = mb[m];
+                for (int j = g + 1; j < sc->nodes[g].skip; ++j) {
+                    if (!is_tri(j)) continue;
+                    MeshBuild::Tri t;
+                    const double* p = sc->prim_data + sc->nodes[j].prim;
+                    for (int a = 0; a < 3; ++a) {
+                        const double v0 = p[FRT_TRI_P1 + a], v1 = v0 + p[FRT_TRI_E1 + a], v2 = v0 + p[FRT_TRI_E2 + a];
+                        t.lo[a] = std::min(v0, std::min(v1, v2));
+                        t.hi[a] = std::max(v0, std::max(v1, v2));
+                        t.c[a] = 0.5 * (t.lo[a] + t.hi[a]);
+                    }
+                    t.node = j;
+                    t.prim = sc->nodes[j].prim;
+                    B.tris.push_back(t);
+                }
+                B.build(0, (int)B.tris.size(), 1);
+            });
+        for (auto& t : pool) t.join();
+    }
+    std::vector<frt::MeshDesc> desc(roots.size());
+    int depth = 0;
+    const int last_root = sc->num_roots > 0 ? sc->roots[sc->num_roots - 1] : -1;
+    for (size_t m = 0; m < roots.size(); ++m) {
+        int rc = 0;
+        desc[m].nodes = upload(h, mb[m].nodes.data(), mb[m].nodes.size(), rc);
+        desc[m].tris = upload(h, mb[m].refs.data(), mb[m].refs.size(), rc);
+        if (rc) return -1;
+        desc[m].root = roots[m];
+        int top = roots[m];
+        while (sc->nodes[top].parent >= 0) top = sc->nodes[top].parent;
+        desc[m].last_root = top == last_root ? 1 : 0;
+        depth = std::max(depth, mb[m].depth);
+        wn[(size_t)roots[m]].op = (int32_t)m + 1;
+    }
+    if (!roots.empty()) {
+        int rc = 0;
+        S.meshes = upload(h, desc.data(), desc.size(), rc);
+        if (rc) return -1;
+        S.num_meshes = (int32_t)roots.size();
+        S.mesh_stack = depth + 1;
+    }
+    return 0;
+}
+
 // walk visit records (frt_traverse.hpp WalkNode) of the flattened tree
 static void build_walk_nodes(const frt_scene* sc, std::vector<frt::WalkNode>& wn) {
     auto invert4 = [](const double* m, double* out) -> bool {  // Gauss-Jordan, partial pivoting
@@ -1720,6 +1954,10 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     {
         std::vector<frt::WalkNode> wn;
         build_walk_nodes(sc, wn);
+        if (rc == 0 && build_meshes(h, sc, wn)) {
+            frt_scene_release(h);
+            return -1;
+        }
         S.wn = upload(h, wn.data(), wn.size(), rc);
         const char* jit_env = std::getenv("FRT_JIT");
         if (rc == 0 && sc->config.include_direct && !(jit_env && std::strcmp(jit_env, "0") == 0)) {
@@ -1825,7 +2063,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         S.comp_depth = comp_depth;
         S.xf_depth = xf_depth;
         S.features = features;
-        h->lds_bytes = (size_t)frt::walk_lds_bytes(list_cap, comp_depth, xf_depth);
+        h->lds_bytes = (size_t)frt::walk_lds_bytes(list_cap, comp_depth, xf_depth, S.mesh_stack);
         if (h->lds_bytes > 64 * 1024) {
             frt_scene_release(h);
             return fail("frt_scene_upload: scene needs " + std::to_string(h->lds_bytes) +

@@ -109,6 +109,22 @@ struct PhotonMapDev {
     double inv_cell;
 };
 
+// A mesh: a group subtree of groups and triangles only (no transforms below its root, no CSG around it)
+// gets a BVH of its own at upload (frt_engine.hip build_meshes): binary32 boxes rounded outward, two
+// children per node, the smallest pre-order index below each child. The walk searches it per lane
+// (mesh_closest / mesh_first) instead of visiting the reference's group tree node by node.
+struct MeshNode {
+    float b[12];        // child 0 lo xyz, hi xyz; child 1 lo xyz, hi xyz
+    int32_t child[2];   // >= 0: node; < 0: leaf, ~child = first << 3 | (count - 1) in tris
+    int32_t mindfs[2];  // the smallest pre-order index of the triangles below each child
+};
+struct MeshDesc {
+    const MeshNode* nodes;  // node 0: the root
+    const int2* tris;       // (pre-order index, prim_data offset) per leaf entry
+    int32_t root;           // the mesh's root group in the node array
+    int32_t last_root;      // inside the last world shape (the shadow search applies)
+};
+
 struct DevScene {
     const WalkNode* __restrict__ wn;
     const frt_node* __restrict__ nodes;
@@ -134,6 +150,9 @@ struct DevScene {
     frt_camera cam;
     frt_config cfg;
     PhotonMapDev pmaps[2];  // 0 caustic, 1 global (global illumination only)
+    const MeshDesc* meshes;  // WalkNode::op - 1 of a mesh's root group (0: not a mesh)
+    int32_t num_meshes;
+    int32_t mesh_stack;      // per-lane LDS stack entries of the mesh searches (0: no meshes)
 };
 
 enum FeatureBits : int { kFeatCsg = 1, kFeatTorus = 2 };
@@ -201,12 +220,14 @@ struct WalkLds {
     int* ca;     // composite frame: CSG mid / group current-child start (per lane)
     int* cn;     // composite frame: node (per wave)
     int* xn;     // transform frame: node (per wave)
+    int* ms;     // mesh search stack (per lane)
     __device__ __forceinline__ double& T(int k) const { return lt[k * kTraceBlock]; }
     __device__ __forceinline__ int& N(int k) const { return ln[k * kTraceBlock]; }
 };
 
-__host__ __device__ constexpr int walk_lds_bytes(int list_cap, int comp_depth, int xf_depth) {
-    return (12 * list_cap + 8 * comp_depth) * kTraceBlock + 4 * (comp_depth + xf_depth) * (kTraceBlock / 64);
+__host__ __device__ constexpr int walk_lds_bytes(int list_cap, int comp_depth, int xf_depth, int mesh_stack = 0) {
+    return (12 * list_cap + 8 * comp_depth + 4 * mesh_stack) * kTraceBlock +
+           4 * (comp_depth + xf_depth) * (kTraceBlock / 64);
 }
 
 __device__ __forceinline__ WalkLds walk_lds(const DevScene& S, char* smem) {
@@ -222,6 +243,7 @@ __device__ __forceinline__ WalkLds walk_lds(const DevScene& S, char* smem) {
     int* wave = ints + (L + 2 * C) * kTraceBlock;
     v.cn = wave + w * C;
     v.xn = wave + (kTraceBlock / 64) * C + w * X;
+    v.ms = wave + (kTraceBlock / 64) * (C + X) + l;
     return v;
 }
 
@@ -341,6 +363,202 @@ struct ContainerTop2 {
 
 __device__ __forceinline__ double node_ni(const DevScene& S, int node) {
     return node >= 0 ? S.materials[S.nodes[node].material].Ni : 1.0;
+}
+
+// ---- mesh searches (MeshDesc) ----
+// The reference visits a group's children only when the ray passes the group's box test; the mesh BVH's
+// boxes contain every triangle (binary32, rounded outward) and its box test below is conservative (it
+// never rejects a box the ray meets), so the triangles it reaches include every triangle the reference
+// reaches; triangle t values come from the reference's own arithmetic (leaf_hits). The search's answer is
+// therefore the reference's answer exactly when its winning triangle is one the reference reaches: every
+// group between the mesh root and the triangle passes the reference's box test (mesh_reachable, the walk's
+// own decision). When it does not (a ray grazing a box, in binary64), or the search's stack overflows, the
+// walk descends the mesh's group tree node by node instead.
+
+// the walk's decision to enter group nd (no transform) with ray r: box32 where it decides, else binary64
+__device__ __forceinline__ bool ref_group_enter(const DevScene& S, const WalkNode& nd, const Ray& r) {
+    Frame32 lf;
+    frame32(r, lf);
+    float tmin32 = -1.0f, tmax32 = 1.0f, err32 = 0.0f;
+    const int dec = (lf.exact || (S.walk_flags & 2)) ? -1 : box32(nd.bb32, nd.bmag, lf, tmin32, tmax32, err32);
+    if (dec >= 0) return dec != 0;
+    if (origin_inside(nd.bbox, r)) return true;
+    double tmin = -1.0, tmax = 1.0;
+    if (S.walk_flags & 2) return box_range(nd.bbox, r, tmin, tmax);
+    double rc[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rc[a] = recip<1>(r.d[a]);
+    return box_decide(nd.bbox, r, rc, tmin, tmax);
+}
+
+__device__ __forceinline__ bool mesh_reachable(const DevScene& S, const MeshDesc& M, int leaf, const Ray& r) {
+    for (int a = S.nodes[leaf].parent; a != M.root && a >= 0; a = S.nodes[a].parent)
+        if (!ref_group_enter(S, S.wn[a], r)) return false;
+    return true;
+}
+
+// the ray in binary32 for the conservative box test: origin, clamped reciprocal direction and the absolute
+// error bound of a slab parameter from the origin's and the reciprocal's roundings
+struct MeshRay {
+    float o[3], inv[3], E;
+};
+
+__device__ __forceinline__ void mesh_ray(const Ray& r, MeshRay& m) {
+    float om = 0.0f, im = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        m.o[a] = (float)r.o[a];
+        const float d = (float)r.d[a];
+        m.inv[a] = fabsf(d) < 1e-30f ? copysignf(1e30f, d) : 1.0f / d;
+        om = fmaxf(om, fabsf(m.o[a]));
+        im = fmaxf(im, fabsf(m.inv[a]));
+    }
+    m.E = 8.0f * 0x1p-24f * om * im;
+}
+
+// child box c of N: may the ray meet it within [0 - slack, tlim]? tnear: its (lowered) entry
+__device__ __forceinline__ bool mesh_box(const float* b, const MeshRay& m, float tlim, float& tnear) {
+    float t0 = -__builtin_huge_valf(), t1 = __builtin_huge_valf();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float x = (b[a] - m.o[a]) * m.inv[a], y = (b[3 + a] - m.o[a]) * m.inv[a];
+        t0 = fmaxf(t0, fminf(x, y));
+        t1 = fminf(t1, fmaxf(x, y));
+    }
+    const float s = fmaf(16.0f * 0x1p-24f, fmaxf(fabsf(t0), fabsf(t1)), m.E);
+    tnear = t0 - s;
+    return t0 - s <= t1 + s && t1 + s >= 0.0f && t0 - s <= tlim;  // (false for NaN)
+}
+
+// closest hit among the mesh's triangles, against (best_t, best) from the walk so far (pre-order ties: the
+// smaller index wins). false: the walk must descend the mesh itself (answer unconfirmed)
+__device__ inline bool mesh_closest(const DevScene& S, const MeshDesc& M, const Ray& r, double& best_t, int& best,
+                                    int* stack) {
+    MeshRay m;
+    mesh_ray(r, m);
+    double ct = best >= 0 ? best_t : __builtin_huge_val();
+    int cn = best >= 0 ? best : 0x7fffffff;
+    bool mine = false;  // the current best is a triangle of this mesh
+    auto tlim = [&]() { return ct < 3e38 ? (float)ct * (1.0f + 32.0f * 0x1p-24f) + m.E : __builtin_huge_valf(); };
+    auto leaf = [&](int ref) {
+        const int code = ~ref, first = code >> 3, cnt = (code & 7) + 1;
+        for (int k = 0; k < cnt; ++k) {
+            const int2 tri = M.tris[first + k];
+            LeafHits H;
+            leaf_hits<false>(FRT_TRIANGLE, S.prim + tri.y, r, H);
+            const double t = H.t.v0;
+            if (H.t.n && t > 0 && (t < ct || (t == ct && tri.x < cn))) {
+                ct = t;
+                cn = tri.x;
+                mine = true;
+            }
+        }
+    };
+    int sp = 0, node = 0;
+    bool ok = true;
+    while (true) {
+        const MeshNode& N = M.nodes[node];
+        const float tl = tlim();
+        float tn0, tn1;
+        const bool h0 = mesh_box(N.b, m, tl, tn0), h1 = mesh_box(N.b + 6, m, tl, tn1);
+        const int c0 = N.child[0], c1 = N.child[1];
+        if (h0 && c0 < 0) leaf(c0);
+        if (h1 && c1 < 0) leaf(c1);
+        const bool g0 = h0 && c0 >= 0, g1 = h1 && c1 >= 0;
+        if (g0 && g1) {
+            const bool near0 = tn0 <= tn1;
+            if (sp >= S.mesh_stack) {
+                ok = false;
+                break;
+            }
+            stack[sp * kTraceBlock] = near0 ? c1 : c0;
+            ++sp;
+            node = near0 ? c0 : c1;
+        } else if (g0) {
+            node = c0;
+        } else if (g1) {
+            node = c1;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = stack[sp * kTraceBlock];
+        }
+    }
+    if (!ok) return false;
+    if (mine) {
+        if (!mesh_reachable(S, M, cn, r)) return false;
+        best_t = ct;
+        best = cn;
+    }
+    return true;
+}
+
+// the shadow walk inside a mesh: it ends at the first triangle in pre-order that the ray reaches with an
+// entry t > 0 (group.c:114-121, every enclosing group stops there): the smallest pre-order index among
+// those. found: such a triangle exists (its index and t); false: the walk must descend the mesh itself
+__device__ inline bool mesh_first(const DevScene& S, const MeshDesc& M, const Ray& r, int& found, double& ft,
+                                  int* stack) {
+    MeshRay m;
+    mesh_ray(r, m);
+    int cn = 0x7fffffff;
+    double ct = 0.0;
+    auto leaf = [&](int ref) {
+        const int code = ~ref, first = code >> 3, cnt = (code & 7) + 1;
+        for (int k = 0; k < cnt; ++k) {
+            const int2 tri = M.tris[first + k];
+            if (tri.x >= cn) continue;
+            LeafHits H;
+            leaf_hits<false>(FRT_TRIANGLE, S.prim + tri.y, r, H);
+            if (H.t.n && !(H.t.v0 <= 0)) {  // the walk's stop rule: an entry that is not <= 0
+                cn = tri.x;
+                ct = H.t.v0;
+            }
+        }
+    };
+    const float inf = __builtin_huge_valf();
+    int sp = 0, node = 0;
+    bool ok = true;
+    while (true) {
+        const MeshNode& N = M.nodes[node];
+        float tn0, tn1;
+        const int c0 = N.child[0], c1 = N.child[1];
+        const bool h0 = N.mindfs[0] < cn && mesh_box(N.b, m, inf, tn0);
+        const bool h1 = N.mindfs[1] < cn && mesh_box(N.b + 6, m, inf, tn1);
+        // children in pre-order of their first triangle; leaves first when they come first
+        const bool first0 = N.mindfs[0] <= N.mindfs[1];
+        if (first0) {
+            if (h0 && c0 < 0) leaf(c0);
+            if (h1 && c1 < 0 && N.mindfs[1] < cn) leaf(c1);
+        } else {
+            if (h1 && c1 < 0) leaf(c1);
+            if (h0 && c0 < 0 && N.mindfs[0] < cn) leaf(c0);
+        }
+        const bool g0 = h0 && c0 >= 0 && N.mindfs[0] < cn, g1 = h1 && c1 >= 0 && N.mindfs[1] < cn;
+        if (g0 && g1) {
+            if (sp >= S.mesh_stack) {
+                ok = false;
+                break;
+            }
+            stack[sp * kTraceBlock] = first0 ? c1 : c0;
+            ++sp;
+            node = first0 ? c0 : c1;
+        } else if (g0) {
+            node = c0;
+        } else if (g1) {
+            node = c1;
+        } else {
+            // pop, skipping entries that can no longer hold an earlier triangle (their mindfs is not kept:
+            // the child's box test runs again when the node is visited)
+            if (sp == 0) break;
+            --sp;
+            node = stack[sp * kTraceBlock];
+        }
+    }
+    if (!ok) return false;
+    found = cn == 0x7fffffff ? -1 : cn;
+    ft = ct;
+    if (found >= 0 && !mesh_reachable(S, M, found, r)) return false;
+    return true;
 }
 
 template <bool kShadow, int kFeat>
@@ -588,6 +806,33 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
 #if FRT_PREFILTER
                     frame_cache(cur, fc);
 #endif
+                }
+                // a mesh (MeshDesc): each entering lane searches its BVH; the wave descends the group tree only
+                // for lanes whose answer the search cannot confirm
+                if (type == FRT_GROUP && nd.op > 0 && cp == 0 && (kShadow || (!cont && !filter_casts))) {
+                    const MeshDesc& M = S.meshes[nd.op - 1];
+                    if (!kShadow || M.last_root) {
+                        bool fb = false;
+                        if (enter) {
+                            if constexpr (!kShadow) {
+                                fb = !mesh_closest(S, M, cur, best_t, best, W.ms);
+                            } else {
+                                int f = -1;
+                                double ft = 0.0;
+                                fb = !mesh_first(S, M, cur, f, ft, W.ms);
+                                if (!fb && f >= 0) {
+                                    any_entry = true;
+                                    result = (ft > 0 && ft < distance && S.casts[f]) ? 1 : 0;
+                                    resume = kDone;
+                                }
+                            }
+                            if (!fb && resume != kDone) resume = nd.skip;
+                        }
+                        if (__ballot(fb) == 0) {
+                            i = nd.skip;
+                            continue;
+                        }
+                    }
                 }
                 if constexpr (kCsg) {
                     if (type == FRT_CSG || cp > 0) {
