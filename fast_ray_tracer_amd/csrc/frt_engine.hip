@@ -32,6 +32,7 @@
 #include <cstring>
 #include <string>
 #include <chrono>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -1594,16 +1595,12 @@ struct MeshBuild {
     }
 };
 
-// the scene's meshes: marks each root in wn (op = mesh index + 1), builds their BVHs (one host thread per
-// mesh), uploads them; S.meshes / num_meshes / mesh_stack
-static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<frt::WalkNode>& wn) {
+// the scene's mesh roots (host): see kMeshMinTris above
+static std::vector<int> mesh_roots(const frt_scene* sc) {
     const int nn = sc->num_nodes;
-    frt::DevScene& S = h->S;
-    S.meshes = nullptr;
-    S.num_meshes = 0;
-    S.mesh_stack = 0;
+    std::vector<int> roots;
     const char* env = std::getenv("FRT_MESH");  // FRT_MESH=0: the plain walk everywhere (A/B runs)
-    if (nn <= 512 || (env && std::strcmp(env, "0") == 0)) return 0;
+    if (nn <= 512 || (env && std::strcmp(env, "0") == 0)) return roots;
     auto is_tri = [&](int i) { return sc->nodes[i].type == FRT_TRIANGLE || sc->nodes[i].type == FRT_SMOOTH_TRIANGLE; };
     // inner[i]: node i may sit inside a mesh (a triangle or a group without transform of such nodes)
     std::vector<char> inner((size_t)nn, 0), in_csg((size_t)nn, 0);
@@ -1627,7 +1624,6 @@ static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<fr
             inner[(size_t)i] = nd.xform < 0 && nd.skip > i + 1 && children_inner(i);
         }
     }
-    std::vector<int> roots;
     for (int i = 0; i < nn; ++i) {
         const frt_node& nd = sc->nodes[i];
         if (nd.type != FRT_GROUP || in_csg[(size_t)i] || nd.skip <= i + 1 || !children_inner(i) ||
@@ -1636,35 +1632,50 @@ static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<fr
         const int par = nd.parent;
         if (par >= 0 && inner[(size_t)i] && sc->nodes[par].type == FRT_GROUP && children_inner(par) &&
             !in_csg[(size_t)par])
-            continue;  // inside a larger mesh
+            continue;  // inside a larger mesh (a root's ancestors are never all inner, so roots do not nest)
         roots.push_back(i);
     }
-    // (a root inside another root cannot happen: a root's ancestors are not all inner)
+    return roots;
+}
+
+// the BVHs of the mesh roots (host; one thread per mesh)
+static std::vector<MeshBuild> mesh_build(const frt_scene* sc, const std::vector<int>& roots) {
     std::vector<MeshBuild> mb(roots.size());
-    {
-        std::vector<std::thread> pool;
-        for (size_t m = 0; m < roots.size(); ++m)
-            pool.emplace_back([&, m]() {
-                const int g = roots[m];
-                MeshBuild& B = mb[m];
-                for (int j = g + 1; j < sc->nodes[g].skip; ++j) {
-                    if (!is_tri(j)) continue;
-                    MeshBuild::Tri t;
-                    const double* p = sc->prim_data + sc->nodes[j].prim;
-                    for (int a = 0; a < 3; ++a) {
-                        const double v0 = p[FRT_TRI_P1 + a], v1 = v0 + p[FRT_TRI_E1 + a], v2 = v0 + p[FRT_TRI_E2 + a];
-                        t.lo[a] = std::min(v0, std::min(v1, v2));
-                        t.hi[a] = std::max(v0, std::max(v1, v2));
-                        t.c[a] = 0.5 * (t.lo[a] + t.hi[a]);
-                    }
-                    t.node = j;
-                    t.prim = sc->nodes[j].prim;
-                    B.tris.push_back(t);
+    std::vector<std::thread> pool;
+    for (size_t m = 0; m < roots.size(); ++m)
+        pool.emplace_back([&, m]() {
+            const int g = roots[m];
+            MeshBuild& B = mb[m];
+            for (int j = g + 1; j < sc->nodes[g].skip; ++j) {
+                if (sc->nodes[j].type != FRT_TRIANGLE && sc->nodes[j].type != FRT_SMOOTH_TRIANGLE) continue;
+                MeshBuild::Tri t;
+                const double* p = sc->prim_data + sc->nodes[j].prim;
+                for (int a = 0; a < 3; ++a) {
+                    const double v0 = p[FRT_TRI_P1 + a], v1 = v0 + p[FRT_TRI_E1 + a], v2 = v0 + p[FRT_TRI_E2 + a];
+                    t.lo[a] = std::min(v0, std::min(v1, v2));
+                    t.hi[a] = std::max(v0, std::max(v1, v2));
+                    t.c[a] = 0.5 * (t.lo[a] + t.hi[a]);
                 }
-                B.build(0, (int)B.tris.size(), 1);
-            });
-        for (auto& t : pool) t.join();
-    }
+                t.node = j;
+                t.prim = sc->nodes[j].prim;
+                B.tris.push_back(t);
+            }
+            B.build(0, (int)B.tris.size(), 1);
+        });
+    for (auto& t : pool) t.join();
+    return mb;
+}
+
+// the scene's meshes: marks each root in wn (op = mesh index + 1), builds and uploads their BVHs;
+// S.meshes / num_meshes / mesh_stack
+static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<frt::WalkNode>& wn) {
+    frt::DevScene& S = h->S;
+    S.meshes = nullptr;
+    S.num_meshes = 0;
+    S.mesh_stack = 0;
+    const std::vector<int> roots = mesh_roots(sc);
+    if (roots.empty()) return 0;
+    std::vector<MeshBuild> mb = mesh_build(sc, roots);
     std::vector<frt::MeshDesc> desc(roots.size());
     int depth = 0;
     const int last_root = sc->num_roots > 0 ? sc->roots[sc->num_roots - 1] : -1;
@@ -1680,13 +1691,11 @@ static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<fr
         depth = std::max(depth, mb[m].depth);
         wn[(size_t)roots[m]].op = (int32_t)m + 1;
     }
-    if (!roots.empty()) {
-        int rc = 0;
-        S.meshes = upload(h, desc.data(), desc.size(), rc);
-        if (rc) return -1;
-        S.num_meshes = (int32_t)roots.size();
-        S.mesh_stack = depth + 1;
-    }
+    int rc = 0;
+    S.meshes = upload(h, desc.data(), desc.size(), rc);
+    if (rc) return -1;
+    S.num_meshes = (int32_t)roots.size();
+    S.mesh_stack = depth + 1;
     return 0;
 }
 
@@ -1912,6 +1921,61 @@ int frt_jit_check(const frt_scene* sc, char* log, size_t log_cap, char* src, siz
     const int rc = frt_jit_compile_only(code, "gfx950", clog);
     put(log, log_cap, clog);
     return rc == 0 ? 0 : -1;
+}
+
+// Diagnostics (host only): the scene's meshes and their BVHs, checked. out[0] meshes, out[1] triangles in
+// them, out[2] BVH nodes, out[3] deepest BVH level. Returns 0 when every BVH is sound (each of the mesh's
+// triangles in exactly one leaf; every child box contains its triangles' vertices and its children's
+// boxes; every child's smallest pre-order index right), else the number of violations.
+int frt_mesh_check(const frt_scene* sc, int64_t* out, int n) {
+    const std::vector<int> roots = mesh_roots(sc);
+    const std::vector<MeshBuild> mb = mesh_build(sc, roots);
+    int64_t stats[4] = {(int64_t)roots.size(), 0, 0, 0};
+    int64_t bad = 0;
+    for (size_t m = 0; m < roots.size(); ++m) {
+        const MeshBuild& B = mb[m];
+        stats[1] += (int64_t)B.tris.size();
+        stats[2] += (int64_t)B.nodes.size();
+        stats[3] = std::max<int64_t>(stats[3], B.depth);
+        std::vector<int> seen((size_t)sc->num_nodes, 0);
+        // (box lo/hi, smallest pre-order index) of a child reference, recursively checked
+        std::function<void(int32_t, const float*, int32_t)> check = [&](int32_t ref, const float* box, int32_t mindfs) {
+            int32_t mn = 0x7fffffff;
+            auto inside = [&](double v, int a) { return (double)box[a] <= v && v <= (double)box[3 + a]; };
+            if (ref < 0) {
+                const int code = ~ref, first = code >> 3, cnt = (code & 7) + 1;
+                for (int k = 0; k < cnt; ++k) {
+                    const int2 t = B.refs[(size_t)(first + k)];
+                    seen[(size_t)t.x]++;
+                    mn = std::min(mn, t.x);
+                    const double* p = sc->prim_data + t.y;
+                    for (int a = 0; a < 3; ++a) {
+                        const double v0 = p[FRT_TRI_P1 + a];
+                        if (!inside(v0, a) || !inside(v0 + p[FRT_TRI_E1 + a], a) || !inside(v0 + p[FRT_TRI_E2 + a], a))
+                            bad++;
+                    }
+                }
+            } else {
+                const frt::MeshNode& N = B.nodes[(size_t)ref];
+                for (int c = 0; c < 2; ++c) {
+                    for (int a = 0; a < 3; ++a)
+                        if (N.b[6 * c + a] < box[a] || N.b[6 * c + 3 + a] > box[3 + a]) bad++;
+                    check(N.child[c], N.b + 6 * c, N.mindfs[c]);
+                    mn = std::min(mn, N.mindfs[c]);
+                }
+            }
+            if (mn != mindfs) bad++;
+        };
+        const float all[6] = {-INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, INFINITY};
+        const frt::MeshNode& R = B.nodes[0];
+        check(0, all, std::min(R.mindfs[0], R.mindfs[1]));
+        for (int j = roots[m] + 1; j < sc->nodes[roots[m]].skip; ++j) {
+            const bool tri = sc->nodes[j].type == FRT_TRIANGLE || sc->nodes[j].type == FRT_SMOOTH_TRIANGLE;
+            if (seen[(size_t)j] != (tri ? 1 : 0)) bad++;
+        }
+    }
+    for (int i = 0; i < n && i < 4; ++i) out[i] = stats[i];
+    return (int)std::min<int64_t>(bad, 1 << 30);
 }
 
 const char* frt_last_error(void) { return g_last_error.c_str(); }

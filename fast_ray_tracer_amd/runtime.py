@@ -258,29 +258,53 @@ def jit_cache_stats() -> dict:
     return dict(zip(("compiles", "disk_hits", "disk_writes", "module_loads", "module_hits"), map(int, out)))
 
 
-def jit_check(scene: Scene) -> tuple[int, str, str]:
-    """Generate and compile (hiprtc, no device needed) the scene-specialised shadow
-    kernel frt_scene_upload would use for this scene: (rc, log, source) with rc 0
-    compiled, 1 not eligible (generic walk), -1 compile error (include/frt_device.h)."""
+def _flat_scene(scene: Scene):
+    """The scene flattened by the host library (frt_flatten_scene); free with frt_flat_scene_free."""
     lib = host_lib()
     vp = ctypes.c_void_p
     lib.frt_flatten_scene.restype = ctypes.c_int
     lib.frt_flatten_scene.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool, vp, ctypes.c_char_p,
                                       ctypes.c_size_t]
     lib.frt_flat_scene_free.argtypes = [vp]
-    lib.frt_jit_check.restype = ctypes.c_int
-    lib.frt_jit_check.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
     fs = ctypes.create_string_buffer(4096)  # frt_scene (a few hundred bytes)
     err = ctypes.create_string_buffer(512)
     if lib.frt_flatten_scene(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter, fs, err, 512):
         raise RuntimeError("frt: flatten failed: " + err.value.decode())
+    return lib, fs
+
+
+def jit_check(scene: Scene) -> tuple[int, str, str]:
+    """Generate and compile (hiprtc, no device needed) the scene-specialised shadow
+    kernel frt_scene_upload would use for this scene: (rc, log, source) with rc 0
+    compiled, 1 not eligible (generic walk), -1 compile error (include/frt_device.h)."""
+    hl, fs = _flat_scene(scene)
+    lib = hl
+    lib.frt_jit_check.restype = ctypes.c_int
+    lib.frt_jit_check.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                  ctypes.c_size_t]
     log = ctypes.create_string_buffer(1 << 16)
     src = ctypes.create_string_buffer(1 << 22)
     try:
         rc = lib.frt_jit_check(fs, log, len(log), src, len(src))
     finally:
-        lib.frt_flat_scene_free(fs)
+        hl.frt_flat_scene_free(fs)
     return rc, log.value.decode(errors="replace"), src.value.decode(errors="replace")
+
+
+def mesh_check(scene: Scene) -> tuple[int, dict]:
+    """The meshes frt_scene_upload would search per lane in BVHs of their own, built
+    and checked on the host (include/frt_device.h frt_mesh_check, no device needed):
+    (violations, {"meshes", "triangles", "bvh_nodes", "depth"})."""
+    hl, fs = _flat_scene(scene)
+    lib = hl
+    lib.frt_mesh_check.restype = ctypes.c_int
+    lib.frt_mesh_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    out = (ctypes.c_int64 * 4)()
+    try:
+        bad = lib.frt_mesh_check(fs, out, 4)
+    finally:
+        hl.frt_flat_scene_free(fs)
+    return bad, dict(zip(("meshes", "triangles", "bvh_nodes", "depth"), map(int, out)))
 
 
 def encode_ppm(rgba: np.ndarray, use_scaling: bool = True) -> bytes:

@@ -249,6 +249,13 @@ void frt_scene_release(frt_scene_handle *h);
  * the compiler log, `src` (may be NULL) the generated HIP source. */
 int frt_jit_check(const frt_scene *scene, char *log, size_t log_cap, char *src, size_t src_cap);
 
+/* Diagnostics (no device needed): the meshes frt_scene_upload would search per lane (group subtrees of
+ * groups and triangles only, scenes over 512 nodes) and their BVHs, checked: every triangle of a mesh
+ * in exactly one leaf, every box containing its triangles' vertices and its children's boxes, every
+ * child's smallest pre-order index right. out[0] meshes, out[1] their triangles, out[2] BVH nodes,
+ * out[3] deepest level (min(n, 4) written). Returns 0 when sound, else the number of violations. */
+int frt_mesh_check(const frt_scene *scene, int64_t *out, int n);
+
 /* Counters of the scene-specialised kernels' code-object cache since the library was loaded (no device
  * needed): out[0] hiprtc compiles, out[1] code objects read from the on-disk cache, out[2] code objects
  * written to it, out[3] modules loaded (one per device and scene source), out[4] uploads that found

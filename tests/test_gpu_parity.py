@@ -216,7 +216,7 @@ def test_jit_compiled_once_and_cached_on_disk(built, tmp_path):
 
 
 def test_gpu_matches_oracle_on_cfg4_rows(built):
-    """cfg4 stand-in: bounding_boxes (6 dragons, 140 951 triangles, BVH) at 800x1000 with a 4x4 CMJ
+    """cfg4 stand-in: bounding_boxes (6 dragons, 140 940 triangles, BVH) at 800x1000 with a 4x4 CMJ
     grid — row bands against the oracle at 1e-4 (the reference is pinned at 100x125x16 by the
     bounding_boxes_100x125_4x4 golden)."""
     import oracle
@@ -269,7 +269,7 @@ def test_mesh_search_equals_generic_walk(built, name):
     """Mesh subtrees (groups of triangles, frt_traverse.hpp MeshDesc) are searched per lane in a BVH of their
     own, closest hit and the shadow walk's first-in-pre-order entry alike; the answer must be the generic
     walk's (which follows the reference's group tree and box tests), every pixel bit for bit. cfg4's
-    stand-in at full size (800x1000, 4x4 CMJ: 6 dragons, 140 951 triangles) and the mesh goldens."""
+    stand-in at full size (800x1000, 4x4 CMJ: 6 dragons, 140 940 triangles) and the mesh goldens."""
     fast = _render_env(name, {"FRT_MESH": "1"})
     plain = _render_env(name, {"FRT_MESH": "0"})
     assert np.array_equal(fast, plain)
