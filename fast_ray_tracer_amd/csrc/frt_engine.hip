@@ -2451,13 +2451,34 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         h->rays_walked += total_mixed * lpp;  // (parts of fewer samples count their padding lanes too)
         h->pairs_walked += total_mixed;
         KTimer tr(h, h->cur_st, 9);
-        for (uint64_t p0 = 0; p0 < total_mixed; p0 += max_pairs) {
-            const uint64_t pc = std::min<uint64_t>(max_pairs, total_mixed - p0);
-            uint32_t total = (uint32_t)(pc * lpp), m0 = (uint32_t)p0;
-            void* args[] = {&h->S, (void*)&B, (void*)&rec, &total, &m0, &h->mixed, &h->mcount, &segcap, &all_pairs,
+        // the mixed pairs' blocks by segment (jit::SegTable); every pair in order without the pair kernel
+        frt::jit::SegTable seg{};
+        uint64_t nblk = 0;
+        for (int j = 0; j < kMixSegs; ++j) {
+            const uint64_t c = all_pairs ? 0 : std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
+            seg.bstart[j] = (uint32_t)nblk;
+            seg.count[j] = (uint32_t)c;
+            nblk += (c * lpp + frt::kTraceBlock - 1) / frt::kTraceBlock;
+        }
+        seg.bstart[kMixSegs] = (uint32_t)nblk;
+        const uint64_t max_blocks = ((1ull << 31) - 1) / frt::kTraceBlock;
+        const uint64_t launches = all_pairs ? (total_mixed + max_pairs - 1) / max_pairs : (nblk + max_blocks - 1) / max_blocks;
+        for (uint64_t li = 0; li < launches; ++li) {
+            uint32_t total = 0, m0 = 0, b0 = 0;
+            uint64_t grid = 0;
+            if (all_pairs) {
+                const uint64_t p0 = li * max_pairs, pc = std::min<uint64_t>(max_pairs, total_mixed - p0);
+                total = (uint32_t)(pc * lpp);
+                m0 = (uint32_t)p0;
+                grid = (total + frt::kTraceBlock - 1) / frt::kTraceBlock;
+            } else {
+                b0 = (uint32_t)(li * max_blocks);
+                grid = std::min<uint64_t>(max_blocks, nblk - b0);
+            }
+            void* args[] = {&h->S, (void*)&B, (void*)&rec, &total, &m0, &h->mixed, &seg, &b0, &segcap, &all_pairs,
                             &h->light_psamp, &lpp, (void*)&magic,
                             &shift, &spn, &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
-            const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, grid_for(total, frt::kTraceBlock),
+            const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, (unsigned)grid,
                                                         1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
             if (le != hipSuccess) {
                 // the pair kernel may have written counts already: clear them and take the generic walk for

@@ -289,6 +289,37 @@ __device__ __forceinline__ void mix_append(bool mix, uint32_t pair, uint32_t val
     }
 }
 
+// The per-ray kernel's blocks by segment (host-built from the segment counts, passed by value): segment
+// s holds count[s] mixed pairs and takes blocks [bstart[s], bstart[s + 1]) of the launch sequence, its
+// pairs' lanes (lpp each) packed over them; a block finds its segment with a scalar binary search.
+struct SegTable {
+    uint32_t bstart[kMixSegs + 1];
+    uint32_t count[kMixSegs];
+};
+
+// (wave-uniform) the segment of global block gb
+__device__ __forceinline__ int seg_of_block(const SegTable& t, uint32_t gb) {
+    int s = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1)
+        if (t.bstart[s + step] <= gb) s += step;  // (s + step <= 63: the table's last entry is never read)
+    return s;
+}
+
+// the lit lanes of each (node, light part) pair: a pair's lanes are lpp consecutive lanes (j = 0..lpp-1),
+// so its head lane (j == 0, or the wave's first lane) adds the pair's lit lanes of this wave
+__device__ __forceinline__ void count_part(const DevScene& S, const Lane32& L, bool lit, uint32_t j, uint32_t lpp,
+                                           int32_t* counts) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lits = __ballot(lit);
+    if (L.valid && (j == 0 || lane == 0)) {
+        const uint32_t len = min(lpp - j, 64u - (uint32_t)lane);
+        const unsigned long long seg = (len >= 64u ? ~0ull : ((1ull << len) - 1ull)) << lane;
+        const int c = __popcll(lits & seg);
+        if (c) atomicAdd(counts + L.node * (uint32_t)S.num_lights + (uint32_t)L.light, c);
+    }
+}
+
 // (all lanes of the wave) mixed index m -> its slot in the segmented list
 __device__ __forceinline__ size_t mix_slot(uint32_t m, const unsigned* __restrict__ mcount, uint32_t segcap) {
     const int lane = threadIdx.x & 63;
@@ -317,23 +348,6 @@ __device__ __forceinline__ void node_stat(unsigned long long* js, int k, bool ac
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(js + 2048 + 2 * k, 1ull);
         atomicAdd(js + 2048 + 2 * k + 1, (unsigned long long)__popcll(m));
-    }
-}
-
-// segmented wave reduction of the lit lanes (shadow_count with 32-bit keys)
-__device__ __forceinline__ void count32(const DevScene& S, const Lane32& L, bool lit, int32_t* counts) {
-    const int lane = threadIdx.x & 63;
-    const int key = L.valid ? (int)(L.node * (uint32_t)S.num_lights) + L.light : -1 - lane;
-    const int prev = __shfl_up(key, 1, 64);
-    const bool head = lane == 0 || prev != key;
-    const unsigned long long heads = __ballot(head);
-    const unsigned long long lits = __ballot(lit);
-    if (L.valid && head) {
-        const unsigned long long above = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
-        const int next = above ? __ffsll((long long)above) - 1 : 64;
-        const unsigned long long seg = (next >= 64 ? ~0ull : ((1ull << next) - 1)) & ~((1ull << lane) - 1);
-        const int c = __popcll(lits & seg);
-        if (c) atomicAdd(counts + key, c);
     }
 }
 
