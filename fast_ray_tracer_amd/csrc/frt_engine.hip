@@ -1313,7 +1313,7 @@ __global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, NodeCols rec, i
 // host side: scene upload, buffer management, frame driver, C ABI
 // ======================================================================
 
-constexpr size_t kJitStatWords = 64 * 32 + 4 * 512;
+constexpr size_t kJitStatWords = 64 * 32 + 2 * 1024 + 2 * 2048;  // per-launch lines, node sites, beam sites
 
 struct frt_scene_handle {
     int device = 0;
@@ -2215,7 +2215,7 @@ void frt_scene_release(frt_scene_handle* h) {
                 if (c[2048 + 2 * k])
                     std::fprintf(stderr, "frt jit stats: node %d: %llu waves, %llu lanes tested; composites: %llu waves, %llu lanes entered\n",
                                  k, c[2048 + 2 * k], c[2048 + 2 * k + 1], c[3072 + 2 * k], c[3072 + 2 * k + 1]);
-            for (int k = std::max(h->S.num_nodes, 100); k < 512; ++k)  // the pair kernel's decision sites (frt_jit.hip)
+            for (int k = std::max(h->S.num_nodes, 100); k < 2048; ++k)  // the pair kernel's decision sites (frt_jit.hip)
                 if (c[3072 + 2 * k + 1])
                     std::fprintf(stderr, "frt jit stats: beam site %d: %llu waves, %llu lanes\n", k, c[3072 + 2 * k],
                                  c[3072 + 2 * k + 1]);

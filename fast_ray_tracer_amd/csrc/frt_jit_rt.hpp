@@ -699,6 +699,24 @@ __device__ __forceinline__ bool sphere_miss32(const Node32& nd, const World32& w
     return c2 > t * t * (1.0f + 16.0f * kU) && vmax < 1e4f * nd.sph[3] && w.omax < 1e8f * nd.sph[3];
 }
 
+// An origin strictly inside an axis-aligned composite's box enters it for every direction: on each axis
+// the reference's slab values are (lo - o'_a) / d'_a < 0 < (hi - o'_a) / d'_a (or -inf / +inf in its
+// EPSILON branch), so tmin < 0 < tmax: a hit, and not behind the ray. The world planes B (binary32, within
+// u |B|), o~ (within u |o|), the subtraction's rounding, the reference's own binary64 roundings and the
+// permutation's remnants (within 2 sigma max|o| in world units) stay inside the margin
+// 8u (max|B| + max|o|) + 2.02 sigma max|o|. World32 and Beam32 (one origin per pair) alike.
+template <int kAa, typename W>
+__device__ __forceinline__ bool inside_aa(const Node32& nd, const W& w) {
+    const float m = fmaf(8.0f * kU, nd.aabmax + w.omax, kAa == 2 ? 2.02f * nd.aasig * w.omax : 0.0f);
+    bool in = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float lo = fminf(nd.aab[a], nd.aab[a + 3]), hi = fmaxf(nd.aab[a], nd.aab[a + 3]);
+        in = in && w.o[a] - lo > m && hi - w.o[a] > m;
+    }
+    return in;
+}
+
 // kAa (per node, fixed by the generator): 0 the node's own frame (frame32i + slab_iv), 1 an
 // axis-aligned frame (aa_slab on the world ray), 2 the same with the permutation's remnants (aasig)
 
