@@ -713,8 +713,52 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     tri_store(surface, i, out);
 }
 
-// bottom-up combine of one level (shade_hit's specular block, renderer.c:773-822)
-// (level 0: samples land in sample_out in sample order, coalesced stores; k_resolve reads each pixel's run)
+// bottom-up combine of one node (shade_hit's specular block, renderer.c:773-822): its A, D, S triples into col
+__device__ __forceinline__ void combine_node(const NodeRec& nr, int64_t i, Cols<Tri9> surface, Cols<Tri9> child,
+                                             const frt_material* __restrict__ mats, int32_t include_specular,
+                                             double* col) {
+    if (nr.material < 0) {
+        for (int k = 0; k < 12; ++k) col[k] = 0.0;
+        return;
+    }
+    tri_load(surface, i, col);
+    if (include_specular) {
+        const frt_material& M = mats[nr.material];
+        // reflected / refracted_color from the children's slots; a child that was not traced
+        // (zero weight, or nothing to spawn) contributes an exact 0
+        double R[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, T[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (nr.flags & kReflSpawned) tri_load(child, 2 * i, R);
+        if (nr.flags & kRefrSpawned) tri_load(child, 2 * i + 1, T);
+        double rl[12], rr[12];
+        for (int t = 0; t < 12; t += 4) {
+            for (int k = 0; k < 3; ++k) {
+                rl[t + k] = (nr.flags & kReflApplies) ? 0.0 + R[t + k] * nr.refl[k] : 0.0;
+                double tt = T[t + k] * M.Tf[k];
+                tt *= nr.over_d;
+                rr[t + k] = (nr.flags & kRefrApplies) ? 0.0 + tt : 0.0;
+            }
+        }
+        if (nr.flags & kMix) {
+            for (int t = 0; t < 12; t += 4) {
+                for (int k = 0; k < 3; ++k) {
+                    rl[t + k] *= nr.rf;
+                    rr[t + k] *= 1.0 - nr.rf;
+                }
+            }
+        }
+        for (int t = 0; t < 12; t += 4)
+            for (int k = 0; k < 3; ++k) col[t + k] += rl[t + k];
+        if (nr.flags & kDissolve)
+            for (int t = 0; t < 12; t += 4)
+                for (int k = 0; k < 3; ++k) col[t + k] *= 1.0 - nr.over_d;
+        for (int t = 0; t < 12; t += 4)
+            for (int k = 0; k < 3; ++k) col[t + k] += rr[t + k];
+    }
+}
+
+// bottom-up combine of one level
+// (level 0 without k_combine_resolve: samples land in sample_out in sample order, coalesced stores; k_resolve
+// reads each pixel's run)
 __global__ void __launch_bounds__(kBlock) k_combine(NodeCols rec, int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
                                                     Cols<Tri9> parent_child, Cols<Tri9> sample_out, int32_t spp,
                                                     const frt_material* __restrict__ mats, int32_t include_specular) {
@@ -722,47 +766,59 @@ __global__ void __launch_bounds__(kBlock) k_combine(NodeCols rec, int64_t n, Col
     if (i >= n) return;
     const NodeRec nr = rec.load(i, mats);
     double col[12];
-    if (nr.material < 0) {
-        for (int k = 0; k < 12; ++k) col[k] = 0.0;
-    } else {
-        tri_load(surface, i, col);
-        if (include_specular) {
-            const frt_material& M = mats[nr.material];
-            // reflected / refracted_color from the children's slots; a child that was not traced
-            // (zero weight, or nothing to spawn) contributes an exact 0
-            double R[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, T[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-            if (nr.flags & kReflSpawned) tri_load(child, 2 * i, R);
-            if (nr.flags & kRefrSpawned) tri_load(child, 2 * i + 1, T);
-            double rl[12], rr[12];
-            for (int t = 0; t < 12; t += 4) {
-                for (int k = 0; k < 3; ++k) {
-                    rl[t + k] = (nr.flags & kReflApplies) ? 0.0 + R[t + k] * nr.refl[k] : 0.0;
-                    double tt = T[t + k] * M.Tf[k];
-                    tt *= nr.over_d;
-                    rr[t + k] = (nr.flags & kRefrApplies) ? 0.0 + tt : 0.0;
-                }
-            }
-            if (nr.flags & kMix) {
-                for (int t = 0; t < 12; t += 4) {
-                    for (int k = 0; k < 3; ++k) {
-                        rl[t + k] *= nr.rf;
-                        rr[t + k] *= 1.0 - nr.rf;
-                    }
-                }
-            }
-            for (int t = 0; t < 12; t += 4)
-                for (int k = 0; k < 3; ++k) col[t + k] += rl[t + k];
-            if (nr.flags & kDissolve)
-                for (int t = 0; t < 12; t += 4)
-                    for (int k = 0; k < 3; ++k) col[t + k] *= 1.0 - nr.over_d;
-            for (int t = 0; t < 12; t += 4)
-                for (int k = 0; k < 3; ++k) col[t + k] += rr[t + k];
-        }
-    }
+    combine_node(nr, i, surface, child, mats, include_specular, col);
     if (nr.parent >= 0) {
         tri_store(parent_child, 2 * (int64_t)nr.parent + nr.slot, col);  // a missed child writes its zeros
     } else {
         tri_store(sample_out, i, col);  // sample order (pixel-major): one coalesced run per column
+    }
+}
+
+// Level 0 combined and resolved in one pass (spp <= kFuseBlock): the level's nodes are the batch's samples
+// in sample order, so a block takes ppb = kFuseBlock / spp whole pixels, one thread per sample, stages the
+// nine A / D / S columns of its samples in LDS and sums each pixel's run in sub-sample order (k_resolve's
+// arithmetic, the same additions in the same order), without the samples' round trip through HBM.
+constexpr int kFuseBlock = 256;
+__global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(NodeCols rec, int64_t n, Cols<Tri9> surface,
+                                                                Cols<Tri9> child, int32_t spp, int32_t ppb,
+                                                                int64_t npix, const frt_material* __restrict__ mats,
+                                                                int32_t include_specular, double* __restrict__ out) {
+    __shared__ double stage[9][kFuseBlock + 1];
+    __shared__ double sum[9][kFuseBlock];
+    const int t = threadIdx.x;
+    const int64_t p0 = (int64_t)blockIdx.x * ppb;
+    const int64_t i = p0 * spp + t;
+    if (t < ppb * spp && i < n) {
+        const NodeRec nr = rec.load(i, mats);
+        double col[12];
+        combine_node(nr, i, surface, child, mats, include_specular, col);
+#pragma unroll
+        for (int f = 0; f < 9; ++f) stage[f][t] = col[(f / 3) * 4 + f % 3];
+    }
+    __syncthreads();
+    for (int q = t; q < ppb * 9; q += kFuseBlock) {
+        const int lp = q / 9, f = q - lp * 9;
+        if (p0 + lp >= npix) continue;
+        const double* st = stage[f] + lp * spp;
+        double acc = 0.0;
+        for (int kk = 0; kk < spp; ++kk) acc += st[kk];
+        sum[f][lp] = acc * (1.0 / (double)spp);
+    }
+    __syncthreads();
+    for (int q = t; q < ppb * 4; q += kFuseBlock) {
+        const int lp = q >> 2, f = q & 3;
+        const int64_t p = p0 + lp;
+        if (p >= npix) continue;
+        double* o = out + 4 * p;
+        if (f == 3) {
+            o[3] = 0.0;
+            continue;
+        }
+        double v = 0.0 + sum[f][lp];  // (A + D + S) / 3 of channel f
+        v += sum[3 + f][lp];
+        v += sum[6 + f][lp];
+        v *= 1.0 / 3.0;
+        o[f] = v;
     }
 }
 
@@ -3211,9 +3267,22 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 else st->primary_rays += (uint64_t)n;
             }
         }
+        // level 0 combined and resolved in one pass when a block holds whole pixels (FRT_FUSE_RESOLVE=0: the
+        // two kernels, A/B runs)
+        const char* fuse_env = std::getenv("FRT_FUSE_RESOLVE");
+        const bool fuse = spp <= kFuseBlock && !(fuse_env && std::strcmp(fuse_env, "0") == 0);
         for (int d = path; d >= 0; --d) {
             const int64_t n = count[d];
             if (n == 0) continue;
+            if (d == 0 && fuse) {
+                KTimer t(h, st, 4);
+                const int32_t ppb = kFuseBlock / spp;
+                hipLaunchKernelGGL(k_combine_resolve, dim3((unsigned)((bp + ppb - 1) / ppb)), dim3(kFuseBlock), 0, h->stream,
+                                   h->levels[0].rec, n, h->levels[0].surface, h->levels[0].child, spp, ppb, bp,
+                                   h->S.materials, h->S.cfg.include_specular, dev_out + 4 * p0);
+                FRT_HIP(hipGetLastError());
+                continue;
+            }
             KTimer t(h, st, 3);
             const Cols<Tri9> parent_child = d > 0 ? h->levels[d - 1].child : Cols<Tri9>{};
             hipLaunchKernelGGL(k_combine, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->levels[d].rec, n,
@@ -3221,7 +3290,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                                h->S.materials, h->S.cfg.include_specular);
             FRT_HIP(hipGetLastError());
         }
-        {
+        if (!fuse) {
             KTimer t(h, st, 4);
             hipLaunchKernelGGL(k_resolve, dim3((unsigned)((bp + 63) / 64)), dim3(kResolveBlock), 0, h->stream, h->sample_col, bp, spp,
                                dev_out + 4 * p0);

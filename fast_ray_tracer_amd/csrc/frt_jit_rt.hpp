@@ -468,12 +468,15 @@ __device__ __forceinline__ bool beam_axis_split(float thr, float bmax, float sig
     const float rs = eN + (kSig ? 1.01f * sig * w.omax : 0.0f);
     const float ds = kSig ? 1.01f * sig * w.Dn : 0.0f;
     const float f = 1.0f - 8.0f * kU;
+    // lower bounds by reciprocal (within 3u of the quotient, inside f), the denominators raised to 2^-100
+    // at least (a larger denominator keeps a lower bound, and no ray moving towards it, 0, becomes a finite
+    // bound in place of +inf)
     if (N0 - rs > 0.0f) {  // below the slab: D_a > 0 moves towards it
-        snear = (N0 - rs) / (fmaxf(w.Dhi[a], 0.0f) + ds) * f;  // (x / 0 = +inf: no ray moves towards it)
+        snear = (N0 - rs) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(w.Dhi[a], 0.0f) + ds, 0x1p-100f)) * f;
         return snear > 0.0f;
     }
     if (-N1 - rs > 0.0f) {  // above
-        snear = (-N1 - rs) / (fmaxf(-w.Dlo[a], 0.0f) + ds) * f;
+        snear = (-N1 - rs) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(-w.Dlo[a], 0.0f) + ds, 0x1p-100f)) * f;
         return snear > 0.0f;
     }
     return false;
@@ -489,10 +492,11 @@ __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, cons
         const float rs = eN + (kSig ? 1.01f * sig * w.omax : 0.0f);
         const float r0 = -N0 - rs, r1 = N1 - rs;
         const float ds = kSig ? 1.01f * sig * w.Dn : 0.0f;
-        const float Mp = fmaxf(w.Dhi[a], 0.0f) + ds, Mn = fmaxf(-w.Dlo[a], 0.0f) + ds;
+        // lower bounds by reciprocal, as in beam_axis_split (no ray of a sign: a finite bound in place of +inf)
+        const float iMp = __builtin_amdgcn_rcpf(fmaxf(fmaxf(w.Dhi[a], 0.0f) + ds, 0x1p-100f));
+        const float iMn = __builtin_amdgcn_rcpf(fmaxf(fmaxf(-w.Dlo[a], 0.0f) + ds, 0x1p-100f));
         const float f = 1.0f - 8.0f * kU;
-        // (x / 0 = +inf: no ray of that sign)
-        const float vmx = fminf(r1 / Mp, r0 / Mn) * f, vmn = fminf(r0 / Mp, r1 / Mn) * f;
+        const float vmx = fminf(r1 * iMp, r0 * iMn) * f, vmn = fminf(r0 * iMp, r1 * iMn) * f;
         mn = Iv{-__builtin_huge_valf(), -vmn};
         mx = Iv{vmx, __builtin_huge_valf()};
         return r0 > 0.0f && r1 > 0.0f && vmx > 0.0f && vmn > 0.0f;  // (false for NaN)
