@@ -380,7 +380,10 @@ __device__ __forceinline__ bool aa_slab(const Node32& nd, const World32& w, Iv& 
         const f2 B = {nd.aab[a], nd.aab[a + 3]};
         const f2 t = __builtin_elementwise_fma(B, f2{w.r[a], w.r[a]}, f2{-w.ro[a], -w.ro[a]});
         const float k1 = kSig ? fmaf(nd.aasig, fabsf(w.r[a]), kAaK1) : kAaK1;
-        const float e = fmaf(fmaxf(fabsf(t.x), fabsf(t.y)), k1, fmaf(nd.aabmax, w.P[a], w.Q[a]));
+        // (the axis' own max|B| bounds its planes' error: slab computations of nodes that share an axis'
+        // planes are the same expressions, which the compiler computes once)
+        const float bm = fmaxf(fabsf(nd.aab[a]), fabsf(nd.aab[a + 3])) * (1.0f + 4.0f * kU);
+        const float e = fmaf(fmaxf(fabsf(t.x), fabsf(t.y)), k1, fmaf(bm, w.P[a], w.Q[a]));
         const f2 m = {fminf(t.x, t.y), fmaxf(t.x, t.y)};
         const f2 l = m - f2{e, e}, h = m + f2{e, e};
         if (a == 0) {
