@@ -1979,6 +1979,35 @@ int frt_jit_check(const frt_scene* sc, char* log, size_t log_cap, char* src, siz
     return rc == 0 ? 0 : -1;
 }
 
+// Diagnostics: sqrt_core / recip_core and normalize3 (frt_math.hpp) against the compiler's sqrt, division
+// and normalize3_ref, bit for bit. Lane i of wave w: components (2u - 1) 2^k, k uniform in [-K, K] with
+// K = 250 on even waves (every squared magnitude in the core range: the fast path) and 320 on odd ones
+// (some out of range: the fallback); the core functions alone on x = m2 and y = sqrt(m2) of in-range lanes.
+__global__ void k_math_selftest(int64_t n, uint64_t seed, unsigned long long* bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;  // (whole waves: n is a multiple of 64)
+    const int K = ((i >> 6) & 1) ? 320 : 250;
+    double v[3];
+    for (int a = 0; a < 3; ++a) {
+        const uint64_t h = frt::mix64(seed ^ frt::mix64((uint64_t)i * 3 + (uint64_t)a + 0x9e3779b97f4a7c15ULL));
+        const double u = (double)(h >> 11) * 0x1.0p-53;
+        const int k = (int)((h & 0x3ff) % (uint64_t)(2 * K + 1)) - K;
+        v[a] = __builtin_ldexp(2.0 * u - 1.0, k);
+    }
+    double r[3], q[3];
+    frt::normalize3(v, r);
+    frt::normalize3_ref(v, q);
+    unsigned long long b = 0;
+    for (int a = 0; a < 3; ++a) b += __double_as_longlong(r[a]) != __double_as_longlong(q[a]);
+    const double m2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    if (m2 >= 0x1p-600 && m2 <= 0x1p600) {
+        const double s = sqrt(m2);
+        b += __double_as_longlong(frt::sqrt_core(m2)) != __double_as_longlong(s);
+        b += __double_as_longlong(frt::recip_core(s)) != __double_as_longlong(1.0 / s);
+    }
+    if (b) atomicAdd(bad, b);
+}
+
 // Diagnostics (host only): the scene's meshes and their BVHs, checked. out[0] meshes, out[1] triangles in
 // them, out[2] BVH nodes, out[3] deepest BVH level. Returns 0 when every BVH is sound (each of the mesh's
 // triangles in exactly one leaf; every child box contains its triangles' vertices and its children's
@@ -2032,6 +2061,22 @@ int frt_mesh_check(const frt_scene* sc, int64_t* out, int n) {
     }
     for (int i = 0; i < n && i < 4; ++i) out[i] = stats[i];
     return (int)std::min<int64_t>(bad, 1 << 30);
+}
+
+// Diagnostics (current device): k_math_selftest over n lanes (rounded up to whole waves); the number of
+// mismatching values, or -1 on a HIP error.
+int64_t frt_math_selftest(int64_t n, uint64_t seed) {
+    n = (std::max<int64_t>(n, 64) + 63) / 64 * 64;
+    unsigned long long* bad = nullptr;
+    if (hipMalloc((void**)&bad, sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long h = 0;
+    bool ok = hipMemset(bad, 0, sizeof(h)) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_math_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, seed, bad);
+        ok = hipGetLastError() == hipSuccess && hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    hip_ignore(hipFree(bad));
+    return ok ? (int64_t)h : -1;
 }
 
 const char* frt_last_error(void) { return g_last_error.c_str(); }

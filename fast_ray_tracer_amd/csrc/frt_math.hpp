@@ -35,9 +35,49 @@ __device__ __forceinline__ double dot3(const double* a, const double* b) {
     return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
 
-// vector_normalize (reference linalg.c:141-148): multiply by the reciprocal
-__device__ __forceinline__ void normalize3(const double* v, double* r) {
+// The compiler's own correctly rounded binary64 sqrt(x) and 1 / y sequences for gfx950 (v_rsq_f64 / v_rcp_f64
+// and their Newton steps, instruction for instruction) without their range steps: sqrt's scaling of
+// x < 2^-767 and its +-0 / +inf pass-through, division's v_div_scale (no scaling: the exponents are far
+// from the limits), v_div_fmas (a plain fma without scaling) and v_div_fixup (no special value, a positive
+// normal quotient). For x in [2^-600, 2^600] (so y = sqrt(x) in [2^-300, 2^300]) they return the same
+// values as sqrt() and 1.0 / y; frt_math_selftest compares them on the device.
+__device__ __forceinline__ double sqrt_core(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double h = x * r, g = r * 0.5;
+    const double e = __builtin_fma(-g, h, 0.5);
+    h = __builtin_fma(h, e, h);
+    g = __builtin_fma(g, e, g);
+    double d = __builtin_fma(-h, h, x);
+    h = __builtin_fma(d, g, h);
+    d = __builtin_fma(-h, h, x);
+    return __builtin_fma(d, g, h);
+}
+__device__ __forceinline__ double recip_core(double y) {
+    double r = __builtin_amdgcn_rcp(y);
+    double e = __builtin_fma(-y, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-y, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double rem = __builtin_fma(-y, r, 1.0);  // (the quotient 1.0 * r is r)
+    return __builtin_fma(rem, r, r);
+}
+
+// vector_normalize (reference linalg.c:141-148): multiply by the reciprocal of the magnitude
+__device__ __forceinline__ void normalize3_ref(const double* v, double* r) {
     double inv = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    double x = v[0], y = v[1], z = v[2];
+    r[0] = x * inv;
+    r[1] = y * inv;
+    r[2] = z * inv;
+}
+// the same values; a wave whose squared magnitudes all lie in [2^-600, 2^600] takes the core sequences
+__device__ __forceinline__ void normalize3(const double* v, double* r) {
+    const double m2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    double inv;
+    if (__ballot(!(m2 >= 0x1p-600 && m2 <= 0x1p600)) == 0ull)
+        inv = recip_core(sqrt_core(m2));
+    else
+        inv = 1.0 / sqrt(m2);
     double x = v[0], y = v[1], z = v[2];
     r[0] = x * inv;
     r[1] = y * inv;

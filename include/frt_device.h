@@ -256,6 +256,11 @@ int frt_jit_check(const frt_scene *scene, char *log, size_t log_cap, char *src, 
  * out[3] deepest level (min(n, 4) written). Returns 0 when sound, else the number of violations. */
 int frt_mesh_check(const frt_scene *scene, int64_t *out, int n);
 
+/* Diagnostics (current device): the engine's binary64 sqrt / reciprocal core sequences and normalize
+ * (frt_math.hpp) against the compiler's sqrt and division on n lanes of random vectors; returns the
+ * number of mismatching values (0: bit-identical), or -1 on a HIP error. */
+int64_t frt_math_selftest(int64_t n, uint64_t seed);
+
 /* Counters of the scene-specialised kernels' code-object cache since the library was loaded (no device
  * needed): out[0] hiprtc compiles, out[1] code objects read from the on-disk cache, out[2] code objects
  * written to it, out[3] modules loaded (one per device and scene source), out[4] uploads that found

@@ -273,3 +273,16 @@ def test_mesh_search_equals_generic_walk(built, name):
     fast = _render_env(name, {"FRT_MESH": "1"})
     plain = _render_env(name, {"FRT_MESH": "0"})
     assert np.array_equal(fast, plain)
+
+
+def test_math_core_sequences_bit_identical(built):
+    """normalize3's core sqrt / reciprocal sequences (frt_math.hpp sqrt_core / recip_core: the compiler's
+    binary64 sequences without their range steps) give the compiler's own sqrt and division results bit for
+    bit, on 4M lanes of vectors spanning 2^-320..2^320 (fast path and fallback waves)."""
+    import ctypes
+    from fast_ray_tracer_amd.runtime import host_lib
+    lib = host_lib()
+    lib.frt_math_selftest.restype = ctypes.c_int64
+    lib.frt_math_selftest.argtypes = [ctypes.c_int64, ctypes.c_uint64]
+    for seed in (1, 0x5eed):
+        assert lib.frt_math_selftest(1 << 22, seed) == 0
