@@ -575,7 +575,7 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                             const double* lp = pts + 3 * p;
                             double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
                             double lv[3];
-                            normalize3(diff, lv);
+                            normalize3_shade(diff, lv);
                             double ldn = dot3(lv, nr.normalv);
                             if (S.cfg.include_diffuse && ldn >= 0.0) {
                                 for (int k = 0; k < 3; ++k) {
@@ -587,9 +587,9 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                             if (S.cfg.include_spec_highlight && ldn >= 0.0) {
                                 double ndl = dot3(nr.normalv, lv);
                                 double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
-                                normalize3(tmp, hv);
+                                normalize3_shade(tmp, hv);
                                 double ndh = fmax(0.0, dot3(nr.normalv, hv));
-                                double edh_inv = 1.0 / fmax(0.0, dot3(nr.eyev, hv));
+                                double edh_inv = recip_shade(fmax(0.0, dot3(nr.eyev, hv)));
                                 double ldh = dot3(lv, hv);
                                 double dist_term = (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
                                 double gc = 2.0 * ndh * edh_inv;
@@ -598,7 +598,7 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                                 // reference's libm pow, like the device pow it replaces
                                 const double om = 1.0 - ldh, om2 = om * om;
                                 double factor = om2 * om2 * om;
-                                double brdf = dist_term * geo / (4.0 * ndl * ned);
+                                double brdf = div_shade(dist_term * geo, 4.0 * ndl * ned);
                                 for (int k = 0; k < 3; ++k) {
                                     double f = nr.Ks[k] + (1.0 - nr.Ks[k]) * factor;
                                     sacc[k] += f * L.intensity[k] * brdf;
@@ -2004,6 +2004,13 @@ __global__ void k_math_selftest(int64_t n, uint64_t seed, unsigned long long* ba
         const double s = sqrt(m2);
         b += __double_as_longlong(frt::sqrt_core(m2)) != __double_as_longlong(s);
         b += __double_as_longlong(frt::recip_core(s)) != __double_as_longlong(1.0 / s);
+        // the shading's approximate reciprocal magnitude: within 2 ulps of 1.0 / sqrt()
+        const double inv = 1.0 / s;
+        const int64_t ulps = __double_as_longlong(frt::rsqrt_nr(m2)) - __double_as_longlong(inv);
+        b += ulps > 2 || ulps < -2;
+        // its exact quotient sequence: a / b for a = |v[0]| + 0 (0 too), b = the magnitude
+        const double a = fabs(v[0]) >= 0x1p-600 ? fabs(v[0]) : 0.0;
+        b += __double_as_longlong(frt::div_shade(a, s)) != __double_as_longlong(a / s);
     }
     if (b) atomicAdd(bad, b);
 }

@@ -84,6 +84,47 @@ __device__ __forceinline__ void normalize3(const double* v, double* r) {
     r[2] = z * inv;
 }
 
+// ---- shading-only approximations (lighting_microfacet's per-light-point terms) ----
+// The reciprocal magnitude of a normalisation from v_rsq_f64 with Newton steps instead of the correctly
+// rounded 1.0 / sqrt(): within 2 ulps of the reference's value (k_math_selftest bounds it on the device),
+// far inside the 1e-4 canvas tolerance; no decision of any walk uses it. A wave takes these when every active lane's
+// operand lies in [2^-600, 2^600] (no overflow, underflow or special value in the steps), else the
+// IEEE operations.
+__device__ __forceinline__ bool wave_in_range(double x) {
+    return __ballot(!(x >= 0x1p-600 && x <= 0x1p600)) == 0ull;
+}
+// 1 / sqrt(x): v_rsq_f64 (~2^-24) and two Newton steps r += r (1/2 - x r^2 / 2)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double t = x * r, g = r * 0.5;
+        r = __builtin_fma(r, __builtin_fma(-g, t, 0.5), r);
+    }
+    return r;
+}
+// vector_normalize (linalg.c:141-148) with the approximate reciprocal magnitude
+__device__ __forceinline__ void normalize3_shade(const double* v, double* r) {
+    const double m2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double inv = wave_in_range(m2) ? rsqrt_nr(m2) : 1.0 / sqrt(m2);
+    r[0] = v[0] * inv;
+    r[1] = v[1] * inv;
+    r[2] = v[2] * inv;
+}
+// 1 / y and a / b (a >= 0) exactly: the compiler's correctly rounded division sequence without its
+// scaling and fix-up steps (recip_core above; for a / b the quotient a r and one residual correction)
+__device__ __forceinline__ double recip_shade(double y) { return wave_in_range(y) ? recip_core(y) : 1.0 / y; }
+__device__ __forceinline__ double div_shade(double a, double b) {
+    if (__ballot(!(b >= 0x1p-600 && b <= 0x1p600 && (a == 0.0 || (a >= 0x1p-600 && a <= 0x1p600)))) == 0ull) {
+        double r = __builtin_amdgcn_rcp(b);
+        r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+        r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+        const double q = a * r;
+        return __builtin_fma(__builtin_fma(-b, q, a), r, q);
+    }
+    return a / b;
+}
+
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {
     double x = a[1] * b[2] - a[2] * b[1];
     double y = a[2] * b[0] - a[0] * b[2];

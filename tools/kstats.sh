@@ -6,7 +6,7 @@ SC=${1:-cornell_direct_800_4x4}
 OUT=$R/gpurun_out/kstats_$SC
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 ${TMO:-300} rocprofv3 --kernel-trace --stats -f csv -d "$OUT" -o run -- python3 "$R/bench.py" --steps ${STEPS:-1} --warmup ${WARMUP:-0} --no-cpu-baseline --scene $SC > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
+timeout -k 10 ${TMO:-300} rocprofv3 --kernel-trace --stats -f csv -d "$OUT" -o run -- python3 "$R/bench.py" --steps ${STEPS:-1} --warmup ${WARMUP:-0} --no-cpu-baseline --scene $SC ${KS_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 f=$(find "$OUT" -name "*kernel_stats.csv" | head -1)
 python3 -c "
 import csv,sys
