@@ -646,13 +646,34 @@ __device__ __forceinline__ bool shade_heavy(const DevScene& S, const int32_t* __
     return false;
 }
 
+// shade_node of a node without light-point work (not shade_heavy): the ambient terms, the same additions
+// (every diffuse / specular term an exact 0)
+__device__ __forceinline__ void ambient_node(const DevScene& S, const NodeRec& nr, double* out) {
+    double sA[3] = {0, 0, 0};
+    if (S.cfg.include_direct && S.cfg.include_ambient)
+        for (int li = 0; li < S.num_lights; ++li) {
+            const frt_light& L = S.lights[li];
+            for (int k = 0; k < 3; ++k) sA[k] += 0.0 + nr.Ka[k] * L.intensity[k];
+        }
+    for (int k = 0; k < 3; ++k) {
+        out[k] = sA[k];
+        out[4 + k] = 0.0;
+        out[8 + k] = 0.0;
+    }
+    out[3] = out[7] = out[11] = 0.0;
+}
+
 // Shading in two kernels: most path nodes of a frame see no light sample at all (cornell 1920x1080: 83 % of
 // the (node, light) pairs are wholly shadowed), and a wave runs its light-point loops whenever one lane
 // needs them. k_shade writes the nodes without light-point work (ambient only) and appends the others to
 // kShadeSegs segments of a list (one atomic per wave on its segment's line); k_shade_lit shades the
 // listed nodes with every lane busy.
+// kLazy (no GI on the surface triples): the nodes without light-point work are not written at all; k_combine
+// computes their ambient terms where it would read them (ambient_node), so k_shade reads only the material
+// and count words.
 constexpr int kShadeSegs = 64;
 static_assert(kShadeSegs == jit::kMixSegs, "k_shade_lit reads its slots with jit::mix_slot");
+template <bool kLazy>
 __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols rec, int64_t n,
                                                   const int32_t* __restrict__ counts, Cols<Tri9> surface,
                                                   uint32_t* __restrict__ lit, unsigned* __restrict__ lcount,
@@ -665,7 +686,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
         mine = nr.material >= 0;
         heavy = mine && lit != nullptr && shade_heavy(S, counts, i);
     }
-    if (mine && !heavy) {
+    if (!kLazy && mine && !heavy) {
         double out[12];
         shade_node(S, B, nr, i, counts, out);
         tri_store(surface, i, out);
@@ -714,14 +735,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
 }
 
 // bottom-up combine of one node (shade_hit's specular block, renderer.c:773-822): its A, D, S triples into col
-__device__ __forceinline__ void combine_node(const NodeRec& nr, int64_t i, Cols<Tri9> surface, Cols<Tri9> child,
+// (counts != nullptr: the surface triples of nodes without light-point work were not written, k_shade<true>)
+__device__ __forceinline__ void combine_node(const DevScene& S, const int32_t* __restrict__ counts,
+                                             const NodeRec& nr, int64_t i, Cols<Tri9> surface, Cols<Tri9> child,
                                              const frt_material* __restrict__ mats, int32_t include_specular,
                                              double* col) {
     if (nr.material < 0) {
         for (int k = 0; k < 12; ++k) col[k] = 0.0;
         return;
     }
-    tri_load(surface, i, col);
+    if (counts != nullptr && !shade_heavy(S, counts, i)) ambient_node(S, nr, col);
+    else tri_load(surface, i, col);
     if (include_specular) {
         const frt_material& M = mats[nr.material];
         // reflected / refracted_color from the children's slots; a child that was not traced
@@ -759,14 +783,15 @@ __device__ __forceinline__ void combine_node(const NodeRec& nr, int64_t i, Cols<
 // bottom-up combine of one level
 // (level 0 without k_combine_resolve: samples land in sample_out in sample order, coalesced stores; k_resolve
 // reads each pixel's run)
-__global__ void __launch_bounds__(kBlock) k_combine(NodeCols rec, int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
+__global__ void __launch_bounds__(kBlock) k_combine(DevScene S, const int32_t* __restrict__ counts, NodeCols rec,
+                                                    int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
                                                     Cols<Tri9> parent_child, Cols<Tri9> sample_out, int32_t spp,
                                                     const frt_material* __restrict__ mats, int32_t include_specular) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const NodeRec nr = rec.load(i, mats);
     double col[12];
-    combine_node(nr, i, surface, child, mats, include_specular, col);
+    combine_node(S, counts, nr, i, surface, child, mats, include_specular, col);
     if (nr.parent >= 0) {
         tri_store(parent_child, 2 * (int64_t)nr.parent + nr.slot, col);  // a missed child writes its zeros
     } else {
@@ -779,7 +804,8 @@ __global__ void __launch_bounds__(kBlock) k_combine(NodeCols rec, int64_t n, Col
 // nine A / D / S columns of its samples in LDS and sums each pixel's run in sub-sample order (k_resolve's
 // arithmetic, the same additions in the same order), without the samples' round trip through HBM.
 constexpr int kFuseBlock = 256;
-__global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(NodeCols rec, int64_t n, Cols<Tri9> surface,
+__global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(DevScene S, const int32_t* __restrict__ counts,
+                                                                NodeCols rec, int64_t n, Cols<Tri9> surface,
                                                                 Cols<Tri9> child, int32_t spp, int32_t ppb,
                                                                 int64_t npix, const frt_material* __restrict__ mats,
                                                                 int32_t include_specular, double* __restrict__ out) {
@@ -791,7 +817,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(NodeCols rec, in
     if (t < ppb * spp && i < n) {
         const NodeRec nr = rec.load(i, mats);
         double col[12];
-        combine_node(nr, i, surface, child, mats, include_specular, col);
+        combine_node(S, counts, nr, i, surface, child, mats, include_specular, col);
 #pragma unroll
         for (int f = 0; f < 9; ++f) stage[f][t] = col[(f / 3) * 4 + f % 3];
     }
@@ -2404,6 +2430,19 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
 
 static inline unsigned grid_for(int64_t n, int block = frt::kBlock) { return (unsigned)((n + block - 1) / block); }
 
+// shading in two kernels (k_shade lists the nodes with light-point work, k_shade_lit shades them);
+// FRT_SHADE_SPLIT=0: one kernel for every node (A/B runs)
+static bool shade_split() {
+    const char* e = std::getenv("FRT_SHADE_SPLIT");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+// the ambient-only nodes' terms computed by k_combine instead of stored by k_shade: with the split and
+// without GI (whose kernels add to the stored surface triples); FRT_SHADE_LAZY=0 stores them (A/B runs)
+static bool shade_lazy(const frt_scene_handle* h) {
+    const char* e = std::getenv("FRT_SHADE_LAZY");
+    return shade_split() && !h->S.cfg.use_gi && !(e && std::strcmp(e, "0") == 0);
+}
+
 // Kernel timing without host synchronisation: events are recorded around each
 // launch on the engine stream and read back once the frame has completed.
 struct KTimer {
@@ -3268,9 +3307,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             }
             {
                 KTimer t(h, st, 2);
-                // (FRT_SHADE_SPLIT=0: one kernel for every node, A/B runs)
-                const char* split_env = std::getenv("FRT_SHADE_SPLIT");
-                const bool split = !(split_env && std::strcmp(split_env, "0") == 0);
+                const bool split = shade_split();
                 const int64_t nblocks = grid_for(n);
                 const uint32_t segcap = (uint32_t)(((nblocks + kShadeSegs - 1) / kShadeSegs) * kBlock);
                 if (split && (grow(&h->shade_lit, h->shade_lit_cap, (int64_t)segcap * kShadeSegs) ||
@@ -3279,8 +3316,12 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 if (split)
                     FRT_HIP(hipMemsetAsync(h->shade_lcount, 0, (size_t)kShadeSegs * jit::kMixLine * sizeof(unsigned),
                                            h->stream));
-                hipLaunchKernelGGL(k_shade, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n, L.counts,
-                                   L.surface, split ? h->shade_lit : nullptr, h->shade_lcount, segcap);
+                if (shade_lazy(h))
+                    hipLaunchKernelGGL(k_shade<true>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
+                                       L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap);
+                else
+                    hipLaunchKernelGGL(k_shade<false>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
+                                       L.counts, L.surface, split ? h->shade_lit : nullptr, h->shade_lcount, segcap);
                 if (split)
                     hipLaunchKernelGGL(k_shade_lit, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec,
                                        L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap);
@@ -3323,6 +3364,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         // two kernels, A/B runs)
         const char* fuse_env = std::getenv("FRT_FUSE_RESOLVE");
         const bool fuse = spp <= kFuseBlock && !(fuse_env && std::strcmp(fuse_env, "0") == 0);
+        const bool lazy = shade_lazy(h);
         for (int d = path; d >= 0; --d) {
             const int64_t n = count[d];
             if (n == 0) continue;
@@ -3330,14 +3372,15 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 KTimer t(h, st, 4);
                 const int32_t ppb = kFuseBlock / spp;
                 hipLaunchKernelGGL(k_combine_resolve, dim3((unsigned)((bp + ppb - 1) / ppb)), dim3(kFuseBlock), 0, h->stream,
-                                   h->levels[0].rec, n, h->levels[0].surface, h->levels[0].child, spp, ppb, bp,
+                                   h->S, lazy ? h->levels[0].counts : nullptr, h->levels[0].rec, n, h->levels[0].surface, h->levels[0].child, spp, ppb, bp,
                                    h->S.materials, h->S.cfg.include_specular, dev_out + 4 * p0);
                 FRT_HIP(hipGetLastError());
                 continue;
             }
             KTimer t(h, st, 3);
             const Cols<Tri9> parent_child = d > 0 ? h->levels[d - 1].child : Cols<Tri9>{};
-            hipLaunchKernelGGL(k_combine, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->levels[d].rec, n,
+            hipLaunchKernelGGL(k_combine, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S,
+                               lazy ? h->levels[d].counts : nullptr, h->levels[d].rec, n,
                                h->levels[d].surface, h->levels[d].child, parent_child, h->sample_col, spp,
                                h->S.materials, h->S.cfg.include_specular);
             FRT_HIP(hipGetLastError());
