@@ -90,8 +90,12 @@ __device__ __forceinline__ void normalize3(const double* v, double* r) {
 // far inside the 1e-4 canvas tolerance; no decision of any walk uses it. A wave takes these when every active lane's
 // operand lies in [2^-600, 2^600] (no overflow, underflow or special value in the steps), else the
 // IEEE operations.
+// (FRT_SHADE_FAST=0 builds: the IEEE operations only, A/B runs)
+#ifndef FRT_SHADE_FAST
+#define FRT_SHADE_FAST 1
+#endif
 __device__ __forceinline__ bool wave_in_range(double x) {
-    return __ballot(!(x >= 0x1p-600 && x <= 0x1p600)) == 0ull;
+    return FRT_SHADE_FAST && __ballot(!(x >= 0x1p-600 && x <= 0x1p600)) == 0ull;
 }
 // 1 / sqrt(x): v_rsq_f64 (~2^-24) and two Newton steps r += r (1/2 - x r^2 / 2)
 __device__ __forceinline__ double rsqrt_nr(double x) {
@@ -115,7 +119,8 @@ __device__ __forceinline__ void normalize3_shade(const double* v, double* r) {
 // scaling and fix-up steps (recip_core above; for a / b the quotient a r and one residual correction)
 __device__ __forceinline__ double recip_shade(double y) { return wave_in_range(y) ? recip_core(y) : 1.0 / y; }
 __device__ __forceinline__ double div_shade(double a, double b) {
-    if (__ballot(!(b >= 0x1p-600 && b <= 0x1p600 && (a == 0.0 || (a >= 0x1p-600 && a <= 0x1p600)))) == 0ull) {
+    if (FRT_SHADE_FAST &&
+        __ballot(!(b >= 0x1p-600 && b <= 0x1p600 && (a == 0.0 || (a >= 0x1p-600 && a <= 0x1p600)))) == 0ull) {
         double r = __builtin_amdgcn_rcp(b);
         r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
         r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);

@@ -210,9 +210,10 @@ def test_jit_compiled_once_and_cached_on_disk(built, tmp_path):
     second = probe()
     print("second process", second)
     assert second["after_handles"]["compiles"] == 0 and second["after_render_multi"]["disk_hits"] == 1
-    # a cold render_multi in a new process: no compile (generous bound: the first hipModuleLoadData and
-    # stream setup of the process)
-    assert second["cold_ms"] <= second["warm_ms"] + 150.0, second
+    # a cold render_multi in a new process: no compile (a gfx950 hiprtc compile of this kernel is ~0.9 s;
+    # the bound leaves room for the process's first module load, allocations and stream setup, which
+    # measured 130-210 ms on different boxes)
+    assert second["cold_ms"] <= second["warm_ms"] + 400.0, second
 
 
 def test_gpu_matches_oracle_on_cfg4_rows(built):
@@ -276,9 +277,10 @@ def test_mesh_search_equals_generic_walk(built, name):
 
 
 def test_math_core_sequences_bit_identical(built):
-    """normalize3's core sqrt / reciprocal sequences (frt_math.hpp sqrt_core / recip_core: the compiler's
-    binary64 sequences without their range steps) give the compiler's own sqrt and division results bit for
-    bit, on 4M lanes of vectors spanning 2^-320..2^320 (fast path and fallback waves)."""
+    """The core binary64 sequences (frt_math.hpp sqrt_core / recip_core / div_shade: the compiler's sequences
+    without their range steps) give the compiler's own sqrt and division results bit for bit — normalize3 and
+    the shading's BRDF quotient — and the shading's approximate reciprocal magnitude (rsqrt_nr) stays within
+    2 ulps, on 4M lanes of vectors spanning 2^-320..2^320 (fast path and fallback waves)."""
     import ctypes
     from fast_ray_tracer_amd.runtime import host_lib
     lib = host_lib()
