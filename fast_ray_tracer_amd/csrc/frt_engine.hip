@@ -570,9 +570,17 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     double ned = 0.0;
                     if (S.cfg.include_spec_highlight) ned = dot3(nr.normalv, nr.eyev);
                     double dacc[3] = {0, 0, 0}, sacc[3] = {0, 0, 0};
+                    // (the next point's load is issued before this point's arithmetic, so its latency hides
+                    // behind the ~700 cycles of binary64 work instead of stalling every iteration)
                     auto points = [&](const double* pts) {
-                        for (int p = 0; p < L.num_samples; ++p) {
-                            const double* lp = pts + 3 * p;
+                        const int ns = L.num_samples;
+                        double nx[3] = {pts[0], pts[1], pts[2]};
+                        for (int p = 0; p < ns; ++p) {
+                            const double lp[3] = {nx[0], nx[1], nx[2]};
+                            const double* q = pts + 3 * min(p + 1, ns - 1);
+                            nx[0] = q[0];
+                            nx[1] = q[1];
+                            nx[2] = q[2];
                             double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
                             double lv[3];
                             normalize3_shade(diff, lv);
