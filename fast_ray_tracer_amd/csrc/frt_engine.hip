@@ -313,8 +313,14 @@ struct HitRec {
 extern __shared__ __align__(16) char frt_walk_smem[];
 
 // closest hit of every ray of one level (level 0: camera rays generated in place)
+// (waves per SIMD asked of the compiler: 4 fit the walk without the torus's quartic in 128 VGPRs without
+// spills, measured 10.1 -> 8.7 ms per headline frame over the compiler's own 3; the torus variants keep theirs)
+#ifndef FRT_TRACE_WAVES
+#define FRT_TRACE_WAVES 4
+#endif
 template <int kFeat>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
+__global__ void __launch_bounds__(kTraceBlock)
+__attribute__((amdgpu_waves_per_eu((kFeat & kFeatTorus) ? 1 : FRT_TRACE_WAVES, 8))) k_trace(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
                                                        HitRec* __restrict__ hits, unsigned* err, int filter_casts) {
     // every lane of the wave takes part in the (wave-coherent) walk; queued rays with
     // parent < -1 are placeholders (final-gather slots of nodes without a gather)
@@ -342,8 +348,12 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(DevScene S, Batch B, cons
 }
 
 // prepare_computations + spawn of the reflection / refraction rays (renderer.c:369-605)
+#ifndef FRT_PREPARE_WAVES
+#define FRT_PREPARE_WAVES 1
+#endif
 template <bool kPat>
-__global__ void __launch_bounds__(kBlock) k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPat ? 1 : FRT_PREPARE_WAVES, 8)))
+k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
                                                     const HitRec* __restrict__ hits, NodeCols rec,
                                                     ShadowHead* __restrict__ heads,
                                                     QueuedRay* __restrict__ next_q,
@@ -713,9 +723,11 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
     }
 }
 
-// the listed nodes (k_shade); one lane each, the grid sized for every node of the level
+// the listed nodes (k_shade); one lane each, the grid sized for every node of the level (4 waves per SIMD asked
+// of the compiler: 128 VGPRs with a few spilled outside the light-point loop, 16.5 -> 15.9 ms per headline
+// frame over its own 3)
 #ifndef FRT_SHADE_WAVES
-#define FRT_SHADE_WAVES 1
+#define FRT_SHADE_WAVES 4
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_SHADE_WAVES, 8))) k_shade_lit(DevScene S, Batch B, NodeCols rec,
                                                       const int32_t* __restrict__ counts, Cols<Tri9> surface,
