@@ -98,7 +98,8 @@ def reference_rays(name: str):
 
 def cpu_baseline() -> dict | None:
     """The reference's own pthread render_multi on this host, on a bounded sample of the workload:
-    the same camera and scene at 240x135 (1/64 of the pixels, 8x8 CMJ), threads = the CPU quota of this process (runtime.cpu_share).
+    the same camera and scene at 240x135 (1/64 of the pixels, 8x8 CMJ), timed with the pool at the CPU quota of
+    this process (runtime.cpu_share) and at os.cpu_count(); the faster run is the baseline, both are reported.
     The binary is oracle/_ref/bin/<sample>: built from the reference's sources by oracle/build_ref.sh
     in the build container (a git-ignored artefact that travels with the working tree; no reference
     source is in the repo). Without it, the repository's own C restatement (oracle/, "port") is timed."""
@@ -110,24 +111,40 @@ def cpu_baseline() -> dict | None:
     # GPU) while os.cpu_count() reports the whole machine (256); more threads than the quota only time-slice
     threads = cpu_share()
     if os.path.exists(exe) and rays:
-        stats = "/tmp/frt_bench_ref_stats_%d.json" % os.getpid()
-        os.makedirs("/tmp/frt_golden/out", exist_ok=True)
-        t0 = time.time()
-        proc = subprocess.run([exe], cwd=ASSETS, env=dict(os.environ, FRT_REF_STATS=stats, FRT_REF_THREADS=str(threads)),
-                              stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, timeout=600)
-        if proc.returncode != 0:
-            log("cpu_baseline: reference run failed:", proc.stderr[-500:])
-            return None
-        st = json.load(open(stats))
-        secs = st["render_multi_seconds"]
-        return {"value": round(rays / secs / 1e6, 4), "unit": "Mrays/s", "cores": int(st["threads"]),
-                "kind": "reference", "threads": int(st["threads"]), "cpu_quota": cpu_share(),
-                "host_cpus_visible": host_cpus, "seconds": round(secs, 3), "wall_seconds": round(time.time() - t0, 3),
-                "sample": "%s: the reference's render_multi (pthread pool, %d threads = this process's CPU quota of "
-                          "the %d CPUs the machine shows) built from /root/reference sources by oracle/build_ref.sh, "
-                          "%dx%dx%d spp (the benchmark camera at 1/64 of the pixels), %d reference rays counted by "
-                          "the oracle" % (CPU_SAMPLE_SCENE, st["threads"], host_cpus, st["width"], st["height"],
-                                          st["usteps"] * st["vsteps"], rays)}
+        def run_ref(nt: int):
+            stats = "/tmp/frt_bench_ref_stats_%d_%d.json" % (os.getpid(), nt)
+            os.makedirs("/tmp/frt_golden/out", exist_ok=True)
+            t0 = time.time()
+            proc = subprocess.run([exe], cwd=ASSETS, env=dict(os.environ, FRT_REF_STATS=stats, FRT_REF_THREADS=str(nt)),
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, timeout=600)
+            if proc.returncode != 0:
+                log("cpu_baseline: reference run failed:", proc.stderr[-500:])
+                return None
+            st = json.load(open(stats))
+            st["wall_seconds"] = time.time() - t0
+            return st
+        # the pool at this process's CPU quota and at every CPU the machine shows (the reference's own
+        # thread-count knob, config.py: threads = CPU count); the faster one is the baseline
+        runs = []
+        for nt in sorted({threads, host_cpus or threads}):
+            st = run_ref(nt)
+            if st is None:
+                return None
+            runs.append(st)
+        best = min(runs, key=lambda r: r["render_multi_seconds"])
+        secs = best["render_multi_seconds"]
+        return {"value": round(rays / secs / 1e6, 4), "unit": "Mrays/s", "cores": int(best["threads"]),
+                "kind": "reference", "threads": int(best["threads"]), "cpu_quota": cpu_share(),
+                "host_cpus_visible": host_cpus, "seconds": round(secs, 3),
+                "wall_seconds": round(best["wall_seconds"], 3),
+                "runs": [{"threads": int(r["threads"]), "value": round(rays / r["render_multi_seconds"] / 1e6, 4),
+                          "seconds": round(r["render_multi_seconds"], 3)} for r in runs],
+                "sample": "%s: the reference's render_multi (pthread pool) built from /root/reference sources by "
+                          "oracle/build_ref.sh, %dx%dx%d spp (the benchmark camera at 1/64 of the pixels), %d "
+                          "reference rays counted by the oracle; timed with %s threads (this process's CPU quota "
+                          "and the %d CPUs the machine shows), the faster reported"
+                          % (CPU_SAMPLE_SCENE, best["width"], best["height"], best["usteps"] * best["vsteps"], rays,
+                             " and ".join(str(int(r["threads"])) for r in runs), host_cpus)}
     # checker leg only (never the GPU path): the oracle restatement on the same sample
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
