@@ -64,13 +64,12 @@ struct NodeRec {
 };
 static_assert(sizeof(NodeRec) == 216, "NodeRec layout");
 
-// NodeRec in HBM: the fields every path node needs (14 column words) and its material colours (13
-// words), which k_prepare stores only for materials with patterns on them (kOwnColors; every other
-// reader takes them from the material table): the colours of pattern-free materials are never written
-// or read per node, and a missed ray writes only its material / parent / slot words.
+// NodeRec in HBM: the fields every path node needs (10 column words), its over_point and key from the
+// node's ShadowHead (which k_prepare writes for the shadow pass anyway: no second copy), and its material
+// colours (13 words), which k_prepare stores only for materials with patterns on them (kOwnColors; every
+// other reader takes them from the material table): the colours of pattern-free materials are never
+// written or read per node, and a missed ray writes only its material / parent / slot words.
 struct NodeCore {
-    double over_point[3];
-    uint64_t key;
     int32_t material, parent, slot, flags;
     double normalv[3], eyev[3];
     double over_d, rf;
@@ -79,12 +78,13 @@ struct NodeColors {
     double Ka[3], Kd[3], Ks[3], refl[3];
     double Ns;
 };
-static_assert(sizeof(NodeCore) == 112 && sizeof(NodeColors) == 104, "NodeCols layout");
+static_assert(sizeof(NodeCore) == 80 && sizeof(NodeColors) == 104, "NodeCols layout");
 enum : int32_t { kOwnColors = 64 };  // (NodeFlags bit) the node's colours are in NodeCols::col
 
 struct NodeCols {
     Cols<NodeCore> core;
     Cols<NodeColors> col;
+    const ShadowHead* head = nullptr;  // over_point, key (the level's ShadowHead array)
     static size_t bytes(int64_t cap) { return Cols<NodeCore>::bytes(cap) + Cols<NodeColors>::bytes(cap); }
     void set(uint64_t* base, int64_t cap) {  // (host) one allocation of bytes(cap)
         core.w = base;
@@ -95,11 +95,9 @@ struct NodeCols {
     __device__ __forceinline__ void store(int64_t i, const NodeRec& v, bool own_colors) const {
         NodeCore c;
         for (int k = 0; k < 3; ++k) {
-            c.over_point[k] = v.over_point[k];
             c.normalv[k] = v.normalv[k];
             c.eyev[k] = v.eyev[k];
         }
-        c.key = v.key;
         c.material = v.material;
         c.parent = v.parent;
         c.slot = v.slot;
@@ -123,18 +121,19 @@ struct NodeCols {
     __device__ __forceinline__ void store_miss(int64_t i, int32_t parent, int32_t slot) const {
         const uint64_t w4 = (uint64_t)(uint32_t)-1 | ((uint64_t)(uint32_t)parent << 32);
         const uint64_t w5 = (uint64_t)(uint32_t)slot;
-        core.w[4 * core.cap + i] = w4;
-        core.w[5 * core.cap + i] = w5;
+        core.w[0 * core.cap + i] = w4;
+        core.w[1 * core.cap + i] = w5;
     }
     __device__ __forceinline__ NodeRec load(int64_t i, const frt_material* __restrict__ mats) const {
         const NodeCore c = core.load(i);
         NodeRec v;
+        const ShadowHead& hd = head[i];  // (dead, and not loaded, where a kernel uses neither field)
         for (int k = 0; k < 3; ++k) {
-            v.over_point[k] = c.over_point[k];
+            v.over_point[k] = hd.over_point[k];
             v.normalv[k] = c.normalv[k];
             v.eyev[k] = c.eyev[k];
         }
-        v.key = c.key;
+        v.key = hd.key;
         v.material = c.material;
         v.parent = c.parent;
         v.slot = c.slot;
@@ -2437,6 +2436,7 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
         L.rec.set((uint64_t*)p, nc);
     }
     FRT_HIP(hipMalloc((void**)&L.head, nc * sizeof(frt::ShadowHead)));
+    L.rec.head = L.head;
     FRT_HIP(hipMalloc((void**)&L.q, nc * sizeof(frt::QueuedRay)));
     FRT_HIP(hipMalloc((void**)&L.surface.w, frt::Cols<frt::Tri9>::bytes(nc)));
     L.surface.cap = nc;
