@@ -2076,13 +2076,13 @@ __global__ void k_math_selftest(int64_t n, uint64_t seed, unsigned long long* ba
         const double s = sqrt(m2);
         b += __double_as_longlong(frt::sqrt_core(m2)) != __double_as_longlong(s);
         b += __double_as_longlong(frt::recip_core(s)) != __double_as_longlong(1.0 / s);
-        // the shading's approximate reciprocal magnitude: within 2 ulps of 1.0 / sqrt()
+        // the shading's approximations (FRT_SHADE_NEWTON steps): reciprocal magnitude, reciprocal and
+        // quotient within 2^-46 relative of 1.0 / sqrt(), 1.0 / y and a / y
         const double inv = 1.0 / s;
-        const int64_t ulps = __double_as_longlong(frt::rsqrt_nr(m2)) - __double_as_longlong(inv);
-        b += ulps > 2 || ulps < -2;
-        // its exact quotient sequence: a / b for a = |v[0]| + 0 (0 too), b = the magnitude
+        b += !(fabs(frt::rsqrt_nr(m2) - inv) <= 0x1p-46 * inv);
+        b += !(fabs(frt::recip_shade(s) - inv) <= 0x1p-46 * inv);
         const double a = fabs(v[0]) >= 0x1p-600 ? fabs(v[0]) : 0.0;
-        b += __double_as_longlong(frt::div_shade(a, s)) != __double_as_longlong(a / s);
+        b += !(fabs(frt::div_shade(a, s) - a / s) <= 0x1p-46 * (a / s));
     }
     if (b) atomicAdd(bad, b);
 }

@@ -85,49 +85,64 @@ __device__ __forceinline__ void normalize3(const double* v, double* r) {
 }
 
 // ---- shading-only approximations (lighting_microfacet's per-light-point terms) ----
-// The reciprocal magnitude of a normalisation from v_rsq_f64 with Newton steps instead of the correctly
-// rounded 1.0 / sqrt(): within 2 ulps of the reference's value (k_math_selftest bounds it on the device),
-// far inside the 1e-4 canvas tolerance; no decision of any walk uses it. A wave takes these when every active lane's
-// operand lies in [2^-600, 2^600] (no overflow, underflow or special value in the steps), else the
-// IEEE operations.
-// (FRT_SHADE_FAST=0 builds: the IEEE operations only, A/B runs)
+// The shading's per-light-point terms (lighting_microfacet) take hardware estimates refined by Newton
+// steps instead of the correctly rounded operations: the reciprocal magnitude of a normalisation from
+// v_rsq_f64, reciprocals and the BRDF quotient from v_rcp_f64, FRT_SHADE_NEWTON steps each (1: relative
+// error below 2^-46, 2: within a few ulps; k_math_selftest bounds them on the device) — far inside the
+// 1e-4 canvas tolerance; no decision of any walk uses them. A lane whose operand lies outside [2^-600,
+// 2^600] (overflow, underflow or a special value in the steps) takes the IEEE operation instead — per
+// lane, so a node's result never depends on which other nodes share its wave (the lit-node list's order
+// is not deterministic). (FRT_SHADE_FAST=0 builds: the IEEE operations only, A/B runs)
 #ifndef FRT_SHADE_FAST
 #define FRT_SHADE_FAST 1
 #endif
-__device__ __forceinline__ bool wave_in_range(double x) {
-    return FRT_SHADE_FAST && __ballot(!(x >= 0x1p-600 && x <= 0x1p600)) == 0ull;
-}
-// 1 / sqrt(x): v_rsq_f64 (~2^-24) and two Newton steps r += r (1/2 - x r^2 / 2)
+#ifndef FRT_SHADE_NEWTON
+#define FRT_SHADE_NEWTON 1
+#endif
+__device__ __forceinline__ bool shade_in_range(double x) { return x >= 0x1p-600 && x <= 0x1p600; }
+// 1 / sqrt(x): v_rsq_f64 (~2^-24) and Newton steps r += r (1/2 - x r^2 / 2)
 __device__ __forceinline__ double rsqrt_nr(double x) {
     double r = __builtin_amdgcn_rsq(x);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < FRT_SHADE_NEWTON; ++k) {
         const double t = x * r, g = r * 0.5;
         r = __builtin_fma(r, __builtin_fma(-g, t, 0.5), r);
     }
     return r;
 }
+// 1 / y: v_rcp_f64 (~2^-24) and Newton steps r += r (1 - y r)
+__device__ __forceinline__ double rcp_nr(double y) {
+    double r = __builtin_amdgcn_rcp(y);
+#pragma unroll
+    for (int k = 0; k < FRT_SHADE_NEWTON; ++k) r = __builtin_fma(r, __builtin_fma(-y, r, 1.0), r);
+    return r;
+}
 // vector_normalize (linalg.c:141-148) with the approximate reciprocal magnitude
 __device__ __forceinline__ void normalize3_shade(const double* v, double* r) {
     const double m2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-    const double inv = wave_in_range(m2) ? rsqrt_nr(m2) : 1.0 / sqrt(m2);
+    double inv;
+    if (FRT_SHADE_FAST) {
+        inv = rsqrt_nr(m2);
+        if (!shade_in_range(m2)) inv = 1.0 / sqrt(m2);  // (divergent: only where some lane needs it)
+    } else {
+        inv = 1.0 / sqrt(m2);
+    }
     r[0] = v[0] * inv;
     r[1] = v[1] * inv;
     r[2] = v[2] * inv;
 }
-// 1 / y and a / b (a >= 0) exactly: the compiler's correctly rounded division sequence without its
-// scaling and fix-up steps (recip_core above; for a / b the quotient a r and one residual correction)
-__device__ __forceinline__ double recip_shade(double y) { return wave_in_range(y) ? recip_core(y) : 1.0 / y; }
+// 1 / y and a / b (a >= 0)
+__device__ __forceinline__ double recip_shade(double y) {
+    if (!FRT_SHADE_FAST) return 1.0 / y;
+    double r = rcp_nr(y);
+    if (!shade_in_range(y)) r = 1.0 / y;
+    return r;
+}
 __device__ __forceinline__ double div_shade(double a, double b) {
-    if (FRT_SHADE_FAST &&
-        __ballot(!(b >= 0x1p-600 && b <= 0x1p600 && (a == 0.0 || (a >= 0x1p-600 && a <= 0x1p600)))) == 0ull) {
-        double r = __builtin_amdgcn_rcp(b);
-        r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
-        r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
-        const double q = a * r;
-        return __builtin_fma(__builtin_fma(-b, q, a), r, q);
-    }
-    return a / b;
+    if (!FRT_SHADE_FAST) return a / b;
+    double q = a * rcp_nr(b);
+    if (!(shade_in_range(b) && (a == 0.0 || shade_in_range(a)))) q = a / b;
+    return q;
 }
 
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {

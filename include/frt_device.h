@@ -257,8 +257,9 @@ int frt_jit_check(const frt_scene *scene, char *log, size_t log_cap, char *src, 
 int frt_mesh_check(const frt_scene *scene, int64_t *out, int n);
 
 /* Diagnostics (current device): the engine's binary64 sqrt / reciprocal core sequences and normalize
- * (frt_math.hpp) against the compiler's sqrt and division on n lanes of random vectors; returns the
- * number of mismatching values (0: bit-identical), or -1 on a HIP error. */
+ * (frt_math.hpp) against the compiler's sqrt and division (bit for bit), and the shading's Newton-refined
+ * estimates against their 2^-46 relative bound, on n lanes of random vectors; returns the number of
+ * failed checks (0: all hold), or -1 on a HIP error. */
 int64_t frt_math_selftest(int64_t n, uint64_t seed);
 
 /* Counters of the scene-specialised kernels' code-object cache since the library was loaded (no device

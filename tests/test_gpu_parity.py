@@ -277,10 +277,10 @@ def test_mesh_search_equals_generic_walk(built, name):
 
 
 def test_math_core_sequences_bit_identical(built):
-    """The core binary64 sequences (frt_math.hpp sqrt_core / recip_core / div_shade: the compiler's sequences
-    without their range steps) give the compiler's own sqrt and division results bit for bit — normalize3 and
-    the shading's BRDF quotient — and the shading's approximate reciprocal magnitude (rsqrt_nr) stays within
-    2 ulps, on 4M lanes of vectors spanning 2^-320..2^320 (fast path and fallback waves)."""
+    """The core binary64 sequences (frt_math.hpp sqrt_core / recip_core: the compiler's sequences without their
+    range steps) give the compiler's own sqrt and division results bit for bit (normalize3), and the
+    shading's Newton-refined estimates (rsqrt_nr, recip_shade, div_shade) stay within 2^-46 relative of the
+    IEEE operations, on 4M lanes of vectors spanning 2^-320..2^320 (fast path and fallback waves)."""
     import ctypes
     from fast_ray_tracer_amd.runtime import host_lib
     lib = host_lib()
