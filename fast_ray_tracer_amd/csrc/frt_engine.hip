@@ -1336,14 +1336,18 @@ constexpr int kGatherReqPerWave = FRT_GATHER_REQ_PER_WAVE;
 // (Tried and measured slower on cornell_gi_480x270_8x8: requests radix-sorted by a Morton key of their point,
 // 1793 -> 1855 ms plus 20 ms of sorting, and with the blocks dealt to the XCDs in contiguous runs 2600 ms:
 // the dense regions then crowd onto one XCD. The estimate is bound by instruction issue, not by L2 misses.)
+// work: nullptr — wave w takes requests [w kGatherReqPerWave, (w + 1) kGatherReqPerWave); else a queue
+// counter: resident waves take kGatherBatch requests at a time until none are left (the dense queries'
+// waves no longer set the launch's tail)
+#ifndef FRT_GATHER_BATCH
+#define FRT_GATHER_BATCH 16
+#endif
+constexpr int kGatherBatch = FRT_GATHER_BATCH;
 __global__ void __launch_bounds__(64 * kGatherWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8)))
-k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col) {
+k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col,
+             unsigned* __restrict__ work) {
     FRT_EST_LDS_W(lds, kGatherEstCap, kGatherWavesPerBlock);
-    const int64_t w = (int64_t)blockIdx.x * kGatherWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t t0 = w * kGatherReqPerWave;
-    for (int j = 0; j < kGatherReqPerWave; ++j) {
-        const int64_t t = t0 + j;
-        if (t >= n) break;
+    auto query = [&](int64_t t) {
         const GatherReq& r = req[t];
         double out3[3] = {0.0, 0.0, 0.0};
         if (r.want) {
@@ -1371,6 +1375,27 @@ k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* _
         }
         if (est_lane() == 0)
             for (int k = 0; k < 3; ++k) gather_col[3 * t + k] = out3[k] * r.jit0;
+    };
+    if (work == nullptr) {
+        const int64_t w = (int64_t)blockIdx.x * kGatherWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int64_t t0 = w * kGatherReqPerWave;
+        for (int j = 0; j < kGatherReqPerWave; ++j) {
+            const int64_t t = t0 + j;
+            if (t >= n) break;
+            query(t);
+        }
+        return;
+    }
+    for (;;) {  // (every wave leaves once the counter passes n)
+        unsigned base = 0;
+        if (est_lane() == 0) base = atomicAdd(work, (unsigned)kGatherBatch);
+        const int64_t t0 = (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(base, 0, 64));
+        if (t0 >= n) break;
+        for (int j = 0; j < kGatherBatch; ++j) {
+            const int64_t t = t0 + j;
+            if (t >= n) break;
+            query(t);
+        }
     }
 }
 
@@ -1527,6 +1552,7 @@ struct frt_scene_handle {
         double* gcol = nullptr;
         frt::GatherReq* greq = nullptr;
         int64_t gq_cap = 0, ghits_cap = 0, gcol_cap = 0, greq_cap = 0;
+        unsigned* gwork = nullptr;  // k_gather_est's queue counter
         double* extra = nullptr;
         double* fgather = nullptr;
         int64_t extra_cap = 0, fgather_cap = 0;
@@ -2425,6 +2451,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(G.ghits));
         hip_ignore(hipFree(G.gcol));
         hip_ignore(hipFree(G.greq));
+        hip_ignore(hipFree(G.gwork));
         hip_ignore(hipFree(G.extra));
         hip_ignore(hipFree(G.fgather));
     }
@@ -3164,9 +3191,24 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
             }
             {
                 KTimer te(h, st, 10);
-                const int64_t gwaves = (rays + kGatherReqPerWave - 1) / kGatherReqPerWave;
-                hipLaunchKernelGGL(k_gather_est, dim3((unsigned)((gwaves + kGatherWavesPerBlock - 1) / kGatherWavesPerBlock)),
-                                   dim3(64 * kGatherWavesPerBlock), 0, h->stream, h->S, G.greq, rays, G.gcol);
+                // FRT_GATHER_QUEUE=0: the static request ranges (A/B runs)
+                const char* qenv = std::getenv("FRT_GATHER_QUEUE");
+                const bool queue = !(qenv && std::strcmp(qenv, "0") == 0) && rays < (int64_t)0xF0000000u;
+                if (queue) {
+                    if (!G.gwork) FRT_HIP(hipMalloc((void**)&G.gwork, sizeof(unsigned)));
+                    FRT_HIP(hipMemsetAsync(G.gwork, 0, sizeof(unsigned), h->stream));
+                    int cus = 0;
+                    FRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+                    // every wave resident at once: FRT_EST_WAVES per SIMD, 4 SIMDs per CU
+                    const int64_t blocks = std::max<int64_t>(1, (int64_t)cus * 4 * FRT_EST_WAVES / kGatherWavesPerBlock);
+                    hipLaunchKernelGGL(k_gather_est, dim3((unsigned)blocks), dim3(64 * kGatherWavesPerBlock), 0, h->stream,
+                                       h->S, G.greq, rays, G.gcol, G.gwork);
+                } else {
+                    const int64_t gwaves = (rays + kGatherReqPerWave - 1) / kGatherReqPerWave;
+                    hipLaunchKernelGGL(k_gather_est, dim3((unsigned)((gwaves + kGatherWavesPerBlock - 1) / kGatherWavesPerBlock)),
+                                       dim3(64 * kGatherWavesPerBlock), 0, h->stream, h->S, G.greq, rays, G.gcol,
+                                       (unsigned*)nullptr);
+                }
             }
             hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
                                G.fgather);
