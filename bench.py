@@ -240,8 +240,10 @@ def gather_roofline(gd: dict) -> dict:
         traffic = 2.0 * t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)
         roof.update({"traffic": round(traffic), "traffic_source": os.path.relpath(path, ROOT),
                      "rocprof_avg_launch_ms": round(t.get("rocprof_avg_ms", 0.0), 4),
-                     "valu_insts_per_query": round(t["SQ_INSTS_VALU_per_launch"] / (64.0 * t["SQ_WAVES_per_launch"]), 1),
-                     "salu_insts_per_query": round(t["SQ_INSTS_SALU_per_launch"] / (64.0 * t["SQ_WAVES_per_launch"]), 1),
+                     # per query: the launch's counts over its queries (the estimate's waves take requests
+                     # from a queue, so waves and queries are not in a fixed ratio)
+                     "valu_insts_per_query": round(t["SQ_INSTS_VALU_per_launch"] / (gd["gather_rays"] / n), 1),
+                     "salu_insts_per_query": round(t["SQ_INSTS_SALU_per_launch"] / (gd["gather_rays"] / n), 1),
                      "wait_any_frac": round(t.get("sq_wait_any_frac_of_wave_cycles", 0.0), 3)})
     return roof
 
