@@ -1376,22 +1376,21 @@ k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* _
         if (est_lane() == 0)
             for (int k = 0; k < 3; ++k) gather_col[3 * t + k] = out3[k] * r.jit0;
     };
-    if (work == nullptr) {
-        const int64_t w = (int64_t)blockIdx.x * kGatherWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        const int64_t t0 = w * kGatherReqPerWave;
-        for (int j = 0; j < kGatherReqPerWave; ++j) {
-            const int64_t t = t0 + j;
-            if (t >= n) break;
-            query(t);
+    // one call site of the estimate (a second one doubles its register pressure: spills)
+    const bool queue = work != nullptr;
+    const int per = queue ? kGatherBatch : kGatherReqPerWave;
+    int64_t t0 = ((int64_t)blockIdx.x * kGatherWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) *
+                 kGatherReqPerWave;
+    for (bool first = true;; first = false) {  // (every wave leaves once the counter passes n)
+        if (queue) {
+            unsigned base = 0;
+            if (est_lane() == 0) base = atomicAdd(work, (unsigned)kGatherBatch);
+            t0 = (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(base, 0, 64));
+        } else if (!first) {
+            break;
         }
-        return;
-    }
-    for (;;) {  // (every wave leaves once the counter passes n)
-        unsigned base = 0;
-        if (est_lane() == 0) base = atomicAdd(work, (unsigned)kGatherBatch);
-        const int64_t t0 = (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(base, 0, 64));
         if (t0 >= n) break;
-        for (int j = 0; j < kGatherBatch; ++j) {
+        for (int j = 0; j < per; ++j) {
             const int64_t t = t0 + j;
             if (t >= n) break;
             query(t);
