@@ -264,6 +264,42 @@ def _render_env(name, env, **kw):
         r.close()
 
 
+def _render_frame_env(name, env, **kw):
+    """Render with environment switches that the engine reads per frame (set around the render only)."""
+    from fast_ray_tracer_amd.runtime import GpuRenderer
+    r = GpuRenderer(load_scene(name))
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return r.render(**kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+        r.close()
+
+
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "reflect_refract_test_150", "patterns_160x80"])
+def test_lazy_ambient_equals_stored_surface(built, name):
+    """Without GI the path nodes no light sample reaches are not written by k_shade: k_combine computes their
+    ambient terms where it would read them (frt_engine.hip ambient_node). The canvas must equal the one with
+    every node's terms stored (FRT_SHADE_LAZY=0), bit for bit — patterned materials (per-node colours) too."""
+    lazy = _render_frame_env(name, {"FRT_SHADE_LAZY": "1"})
+    stored = _render_frame_env(name, {"FRT_SHADE_LAZY": "0"})
+    assert np.array_equal(lazy, stored)
+
+
+def test_gather_queue_equals_static_ranges(built):
+    """The final-gather estimate's request queue (k_gather_est's work counter) only schedules: the GI canvas
+    at one seed must equal the one with fixed request ranges per wave (FRT_GATHER_QUEUE=0), bit for bit."""
+    queued = _render_frame_env("cornell_gi_24", {"FRT_GATHER_QUEUE": "1"})
+    ranges = _render_frame_env("cornell_gi_24", {"FRT_GATHER_QUEUE": "0"})
+    assert np.isfinite(queued).all()
+    assert np.array_equal(queued, ranges)
+
+
 @pytest.mark.parametrize("name", ["bounding_boxes_800x1000_4x4", "bounding_boxes_100x125_4x4", "teapot_low_100",
                                   "nave_120x150_4x4"])
 def test_mesh_search_equals_generic_walk(built, name):
