@@ -58,6 +58,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 2 cycles (SIMD32; binary64
 # and transcendental instructions take 2-4x: profiles/r01_microbench_valu.txt) at the 2.4 GHz peak clock
 VALU_PEAK_GINST_S = 1024 * 2.4 / 2.0
+# SALU issue peak: one scalar unit per CU, one instruction per cycle, shared by the CU's 4 SIMDs
+SALU_PEAK_GINST_S = 256 * 2.4
 
 # algorithmic HBM bytes of the shadow kernel ("byte model"), reported by the engine per frame
 # as stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point, key,
@@ -96,10 +98,12 @@ def reference_rays(name: str):
         return json.load(f).get(name, {}).get("reference_rays", {}).get("total")
 
 
-def cpu_baseline() -> dict | None:
+def cpu_baseline(all_threads: bool = False) -> dict | None:
     """The reference's own pthread render_multi on this host, on a bounded sample of the workload:
     the same camera and scene at 240x135 (1/64 of the pixels, 8x8 CMJ), timed with the pool at the CPU quota of
-    this process (runtime.cpu_share) and at os.cpu_count(); the faster run is the baseline, both are reported.
+    this process (runtime.cpu_share); with all_threads (--cpu-all-threads) also at os.cpu_count() (the
+    reference's own default of one thread per visible CPU: 256 on the GPU box, time-sliced on its 16-CPU
+    quota, measured 4.6x slower in round 3), the faster run being the baseline.
     The binary is oracle/_ref/bin/<sample>: built from the reference's sources by oracle/build_ref.sh
     in the build container (a git-ignored artefact that travels with the working tree; no reference
     source is in the repo). Without it, the repository's own C restatement (oracle/, "port") is timed."""
@@ -126,7 +130,7 @@ def cpu_baseline() -> dict | None:
         # the pool at this process's CPU quota and at every CPU the machine shows (the reference's own
         # thread-count knob, config.py: threads = CPU count); the faster one is the baseline
         runs = []
-        for nt in sorted({threads, host_cpus or threads}):
+        for nt in sorted({threads, host_cpus or threads} if all_threads else {threads}):
             st = run_ref(nt)
             if st is None:
                 return None
@@ -141,10 +145,11 @@ def cpu_baseline() -> dict | None:
                           "seconds": round(r["render_multi_seconds"], 3)} for r in runs],
                 "sample": "%s: the reference's render_multi (pthread pool) built from /root/reference sources by "
                           "oracle/build_ref.sh, %dx%dx%d spp (the benchmark camera at 1/64 of the pixels), %d "
-                          "reference rays counted by the oracle; timed with %s threads (this process's CPU quota "
-                          "and the %d CPUs the machine shows), the faster reported"
+                          "reference rays counted by the oracle; timed with %s threads (this process's CPU quota%s), "
+                          "the faster reported"
                           % (CPU_SAMPLE_SCENE, best["width"], best["height"], best["usteps"] * best["vsteps"], rays,
-                             " and ".join(str(int(r["threads"])) for r in runs), host_cpus)}
+                             " and ".join(str(int(r["threads"])) for r in runs),
+                             " and the %d CPUs the machine shows" % host_cpus if all_threads else "")}
     # checker leg only (never the GPU path): the oracle restatement on the same sample
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -174,9 +179,32 @@ def latest_pmc(kernel: str, workload: str):
     return best
 
 
+def issue_block(t: dict, avg_ms: float, units_per_launch: float, unit_name: str) -> dict:
+    """VALU and SALU issue rates of one kernel from its committed PMC pass (instructions per launch) over
+    the live event-timed launch duration, against the chip's issue peaks."""
+    out = {}
+    for key, peak, name in (("SQ_INSTS_VALU_per_launch", VALU_PEAK_GINST_S, "valu"),
+                            ("SQ_INSTS_SALU_per_launch", SALU_PEAK_GINST_S, "salu")):
+        if key in t:
+            ginst = t[key] / (avg_ms * 1e-3) / 1e9
+            out[name] = {"achieved": round(ginst, 1), "peak": round(peak, 1), "unit": "G wave64 inst/s",
+                         "frac": round(ginst / peak, 3),
+                         "inst_per_64_" + unit_name: round(64.0 * t[key] / units_per_launch, 1) if units_per_launch else None}
+    for k in ("sq_wait_any_frac_of_wave_cycles", "sq_wait_inst_any_frac_of_wave_cycles",
+              "sq_active_inst_any_frac_of_wave_cycles"):
+        if k in t:
+            out[k] = round(t[k], 3)
+    return out
+
+
 def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> dict:
     """The per-ray shadow kernel (frt_jit_shadow; the generic k_shadow when the scene is not eligible),
-    timed by HIP events around its own launches (frt_frame_stats.sub_ms)."""
+    timed by HIP events around its own launches (frt_frame_stats.sub_ms).
+
+    bound: "valu-issue" — the kernel moves few bytes (achieved / peak / frac below are its algorithmic
+    HBM bytes against the 8 TB/s peak, as the bench contract asks) and is limited by instruction issue on
+    both pipes; `issue` holds the VALU and SALU rates from the committed PMC pass of the same kernel on
+    the same workload over the live launch time (and the same for the pair kernel, frt_jit_beam)."""
     if d.get("shadow_jit") and d.get("sub_launches", {}).get("frt_jit_shadow"):
         kname = "frt_jit_shadow"
         avg_ms = d["sub_ms"]["frt_jit_shadow"] / d["sub_launches"]["frt_jit_shadow"]
@@ -187,7 +215,8 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
         nl = max(1, launches["shadow"])
     per_launch = d["shadow_kernel_bytes"] / nl
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    roof = {"bound": "valu-issue" if kname == "frt_jit_shadow" else "hbm", "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kname,
             "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": nl,
             "algorithmic_bytes_per_launch": round(per_launch),
@@ -202,11 +231,17 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
         roof["traffic_source"] = os.path.relpath(path, ROOT)
         if "rocprof_avg_ms" in t:
             roof["rocprof_avg_launch_ms"] = round(t["rocprof_avg_ms"], 4)
-        if "SQ_INSTS_VALU_per_launch" in t:
-            ginst = t["SQ_INSTS_VALU_per_launch"] / (avg_ms * 1e-3) / 1e9
-            roof["valu"] = {"achieved": round(ginst, 1), "peak": VALU_PEAK_GINST_S, "unit": "G wave64 VALU inst/s",
-                            "frac": round(ginst / VALU_PEAK_GINST_S, 3),
-                            "valu_inst_per_64_rays": round(t.get("valu_insts_per_wave", 0), 1)}
+        rays_per_launch = (d.get("shadow_rays_walked") or 0) / nl
+        roof["issue"] = {kname: issue_block(t, avg_ms, rays_per_launch, "rays")}
+        roof["issue"][kname]["source"] = os.path.relpath(path, ROOT)
+    nb = d.get("sub_launches", {}).get("frt_jit_beam")
+    fb = latest_pmc("frt_jit_beam", workload)
+    if nb and fb:
+        bavg = d["sub_ms"]["frt_jit_beam"] / nb
+        pairs_per_launch = (d.get("shadow_pairs") or 0) / nb
+        roof.setdefault("issue", {})["frt_jit_beam"] = dict(issue_block(fb[1], bavg, pairs_per_launch, "pairs"),
+                                                            avg_launch_ms=round(bavg, 4),
+                                                            source=os.path.relpath(fb[0], ROOT))
     return roof
 
 
@@ -220,8 +255,12 @@ def gather_roofline(gd: dict) -> dict:
     the same workload (profiles/r03_pmc_k_gather_est_cornell_gi_1920x1080_8x8.json)."""
     n = gd["sub_launches"]["k_gather_est"]
     avg_ms = gd["sub_ms"]["k_gather_est"] / n
-    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-            "kernel": "k_gather_est", "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": n}
+    roof = {"bound": "latency", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+            "kernel": "k_gather_est", "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": n,
+            "bytes_model": "L2-request bytes: the byte model counts every byte the estimate requests from the memory "
+                           "system (candidate positions, photon records, request, result); the ~100 MB photon map stays "
+                           "in L2 / Infinity Cache, so this is not HBM traffic and frac is not an HBM fraction. The "
+                           "kernel is bound by each query's chain of dependent round trips (wait_any_frac)"}
     model = os.path.join(ROOT, "profiles", "r03_gi_estimate_counters.json")
     if os.path.exists(model):
         m = json.load(open(model))
@@ -248,6 +287,34 @@ def gather_roofline(gd: dict) -> dict:
     return roof
 
 
+def scaling_proxy(renderer, shard, height: int, frame_ms_1: float, ns=(2, 4, 8), reps: int = 2, seed_of=None) -> dict:
+    """The multi-GPU split measured on this one GPU: for N ranks, rank r renders rows r, r + N, ... (the
+    interleave of dist.py / render_multi); ranks 0 and N - 1 (the first and last row sets) are timed on their
+    own, the best of `reps` runs each, and the predicted efficiency is frame_ms_1 / (N x the slower rank).
+    What it leaves out: the canvas gather over RCCL (66 MB per 1920x1080 frame over xGMI, ~1 ms) and any
+    interference between GPUs. seed_of(n, r, i): a seed per run (the GI workload: a photon pass in every run,
+    as every rank of a real run traces its own maps)."""
+    import torch
+    out = {}
+    for n in ns:
+        ms = {}
+        for r in sorted({0, n - 1}):
+            best = None
+            for i in range(reps):
+                seed = seed_of(n, r, i) if seed_of else 0x5EED
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                renderer.render_into(shard.data_ptr(), row_begin=r, row_end=height, row_stride=n, seed=seed)
+                torch.cuda.synchronize()
+                t = 1e3 * (time.perf_counter() - t0)
+                best = t if best is None else min(best, t)
+            ms[r] = best
+        mx = max(ms.values())
+        out[str(n)] = {"rank_ms": {str(k): round(v, 3) for k, v in ms.items()}, "max_rank_ms": round(mx, 3),
+                       "predicted_efficiency": round(frame_ms_1 / (n * mx), 4)}
+    return out
+
+
 def heartbeat(period_s: float = 60.0) -> None:
     """A progress line on stderr every minute while the bench runs (long profiled runs print nothing else)."""
     import threading
@@ -271,6 +338,11 @@ def main():
     ap.add_argument("--batch-samples", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-render-multi", action="store_true", help="skip the drop-in entry point timing")
+    ap.add_argument("--no-scaling-proxy", action="store_true", help="skip the one-GPU proxy of the N-rank split")
+    ap.add_argument("--no-gi-proxy", dest="gi_proxy", action="store_false",
+                    help="skip the GI workload's scaling proxy (about 1.75 GI frames)")
+    ap.add_argument("--cpu-all-threads", action="store_true",
+                    help="also time the reference's pool at os.cpu_count() threads (256 on the GPU box)")
     args = ap.parse_args()
     launch_ranks_if_needed(args)
     heartbeat()
@@ -310,24 +382,29 @@ def main():
     # once warm, on device 0 only (rank 0 of a 1-rank run; outside the timed region)
     rm = {}
     if world == 1 and not args.no_render_multi:
+        from fast_ray_tracer_amd.runtime import render_multi_phases
         torch.cuda.init()
         for key in ("render_multi_wall_ms", "render_multi_wall_ms_warm"):
             t0 = time.perf_counter()
             render_multi(scene, devices=str(local_rank))
             rm[key] = round(1e3 * (time.perf_counter() - t0), 2)
+            rm[key.replace("wall_ms", "phases")] = render_multi_phases()
         # a second process's first render_multi: the scene kernel's code object comes from the on-disk cache
-        # the first call wrote (frt_jit.hip), so no hiprtc compile
-        probe = ("import sys, time; sys.path.insert(0, %r); from fast_ray_tracer_amd import build as b; "
-                 "from fast_ray_tracer_amd.runtime import Scene, render_multi, jit_cache_stats; "
+        # the first call wrote (frt_jit.hip), so no hiprtc compile; its phases say where the rest goes
+        probe = ("import sys, time, json; sys.path.insert(0, %r); from fast_ray_tracer_amd import build as b; "
+                 "from fast_ray_tracer_amd.runtime import Scene, render_multi, jit_cache_stats, render_multi_phases; "
                  "sc = Scene(b.build_scene(%r), asset_root=%r); t0 = time.perf_counter(); "
                  "render_multi(sc, devices=%r); print('RM', 1e3 * (time.perf_counter() - t0), "
-                 "jit_cache_stats()['compiles'])" % (ROOT, os.path.join(GOLDEN, "scenes", args.scene + ".c"), ASSETS,
-                                                      str(local_rank)))
+                 "jit_cache_stats()['compiles']); print('PH', json.dumps(render_multi_phases()))"
+                 % (ROOT, os.path.join(GOLDEN, "scenes", args.scene + ".c"), ASSETS, str(local_rank)))
         pr = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, timeout=300)
         lines = [ln.split() for ln in pr.stdout.splitlines() if ln.startswith("RM ")]
         if pr.returncode == 0 and lines:
             rm["render_multi_wall_ms_second_process"] = round(float(lines[-1][1]), 2)
             rm["render_multi_second_process_compiles"] = int(lines[-1][2])
+            ph = [ln[3:] for ln in pr.stdout.splitlines() if ln.startswith("PH ")]
+            if ph:
+                rm["render_multi_phases_second_process"] = json.loads(ph[-1])
         ndev = torch.cuda.device_count()
         if ndev > 1:  # the in-process multi-GPU path of render_multi (one host thread per device)
             t0 = time.perf_counter()
@@ -367,6 +444,7 @@ def main():
     kernel_ms = dict(d["kernel_ms"])
     launches = dict(d["kernel_launches"])
     traced = (d["primary_rays"] + d["secondary_rays"] + d["shadow_rays"]) * args.steps
+    walked_rays = d["primary_rays"] + d["secondary_rays"] + d.get("shadow_rays_walked", d["shadow_rays"])
 
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     rays = torch.tensor([float(traced)], dtype=torch.float64, device="cuda")
@@ -375,6 +453,9 @@ def main():
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
     t_max = float(t.item())
     total_rays = float(rays.item())
+    proxy = None
+    if world == 1 and not args.no_scaling_proxy:
+        proxy = {"headline": scaling_proxy(renderer, shard, H, 1e3 * t_max / args.steps)}
     renderer.close()
     del shard
 
@@ -412,6 +493,9 @@ def main():
               "kernel_ms_per_frame": {k: round(v, 3) for k, v in gd["kernel_ms"].items()},
               "data": "reference codegen main.c of scenes/cornell_box as shipped (GI on, 65535-row light cache, "
                       "jitter off) with the camera at 1920x1080x64; statistical parity (tests/test_gpu_stochastic.py)"}
+        if world == 1 and not args.no_scaling_proxy and proxy is not None and args.gi_proxy:
+            proxy["gi"] = scaling_proxy(gr, gshard, gscene.height, gi["ms_per_step"], reps=1,
+                                        seed_of=lambda n, r, i: 0x62000 + 16 * n + r)
         if gd.get("sub_launches", {}).get("k_gather_est"):
             gi["gather_est"] = {"ms_per_frame": round(gd["sub_ms"]["k_gather_est"], 3),
                                 "launches": gd["sub_launches"]["k_gather_est"],
@@ -448,6 +532,10 @@ def main():
             "config": {"workload": args.scene, "width": W, "height": H, "spp": scene.spp,
                        "path_length": 5, "parallelism": "rows%d" % world},
             "rays_per_frame_traced": total_rays / args.steps,
+            # rays walked one by one (primary + secondary + the shadow rays of the pairs the pair kernels could
+            # not decide): `value` counts every shadow ray, also those decided for a whole beam at once
+            "rays_per_frame_walked": walked_rays,
+            "walked_mrays_s": round(walked_rays * world * args.steps / t_max / 1e6, 3),
             "reference_equivalent_rays_per_frame": ref_rays,
             "reference_equivalent_mrays_s": round(ref_rays * args.steps / t_max / 1e6, 3) if ref_rays else None,
             "kernel_ms_per_frame": {k: round(v, 4) for k, v in kernel_ms.items()},
@@ -457,6 +545,12 @@ def main():
                                          if k in ("frt_jit_beam", "frt_jit_shadow")},
                 "shadow_rays_per_frame": d["shadow_rays"],
                 "shadow_rays_walked_per_ray": d.get("shadow_rays_walked"),
+                "tile_pairs": d.get("shadow_tile_pairs"), "tile_pairs_mixed": d.get("shadow_tile_mixed"),
+                "node_pairs": d.get("shadow_pairs"), "node_pairs_mixed": d.get("shadow_pairs_mixed"),
+                # the fraction of all shadow rays walked one by one (those of the (node, light part) pairs left
+                # mixed after the tile and node pair kernels)
+                "rays_walked_frac": (round(d["shadow_rays_walked"] / d["shadow_rays"], 4)
+                                     if d.get("shadow_rays") else None),
                 "note": "every shadow ray's occlusion is computed exactly (bit-identical to a per-ray walk, "
                         "tests/test_jit.py); frt_jit_beam resolves whole (path node, light part) pairs by interval "
                         "bounds over all their rays, frt_jit_shadow walks the rays of the pairs it cannot decide"},
@@ -465,8 +559,13 @@ def main():
         out.update(rm)
         if gi is not None:
             out["gi"] = gi
+        if proxy is not None:
+            proxy["note"] = ("one GPU timing the row sets ranks 0 and N-1 of an N-rank run render (bench.py "
+                             "scaling_proxy); predicted_efficiency = the N=1 frame / (N x the slower rank); the RCCL "
+                             "canvas gather (~1 ms per 1920x1080 frame) is not included")
+            out["scaling_proxy"] = proxy
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline()
+            out["cpu_baseline"] = cpu_baseline(all_threads=args.cpu_all_threads)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

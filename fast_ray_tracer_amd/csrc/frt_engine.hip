@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -350,17 +351,15 @@ __attribute__((amdgpu_waves_per_eu((kFeat & kFeatTorus) ? 1 : FRT_TRACE_WAVES, 8
 #ifndef FRT_PREPARE_WAVES
 #define FRT_PREPARE_WAVES 1
 #endif
+// (one path node; returns whether it has a hit, its over_point in op)
 template <bool kPat>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPat ? 1 : FRT_PREPARE_WAVES, 8)))
-k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
-                                                    const HitRec* __restrict__ hits, NodeCols rec,
-                                                    ShadowHead* __restrict__ heads,
-                                                    QueuedRay* __restrict__ next_q,
-                                                    unsigned long long* counters, unsigned* err) {
+__device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, const QueuedRay* __restrict__ q,
+                                             int64_t n, const HitRec* __restrict__ hits, NodeCols& rec,
+                                             ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q,
+                                             unsigned long long* counters, unsigned* err, int64_t node, double* op) {
     // this block's counter line: next-level queue segment count (word level + 1), pruned (16), hits (17)
     unsigned long long* line = counters + kCounterLine * (blockIdx.x % kQueueSegs);
     const int64_t seg_base = (int64_t)(blockIdx.x % kQueueSegs) * B.next_segcap;
-    const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 #ifdef FRT_WALK_PROF
     unsigned long long pt0 = prof_stamp();
     auto pstamp = [&](int k) {
@@ -372,7 +371,6 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
 #else
 #define PSTAMP(k)
 #endif
-    if (node >= n) return;
     Ray r;
     uint64_t key;
     int32_t parent = -1, slot = 0;
@@ -395,7 +393,7 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
     if (hr.node < 0) {
         rec.store_miss(node, parent, slot);
         heads[node].material = -1;
-        return;
+        return false;
     }
     Hit h{hr.t, -1, -1, hr.node};
     Comps c;
@@ -506,6 +504,47 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
     hd.pad = 0;
     heads[node] = hd;
     PSTAMP(4);
+    for (int k = 0; k < 3; ++k) op[k] = c.over_point[k];
+    return true;
+}
+
+// the box of the over_points of a tile's path nodes (tile_log2 of them, consecutive lanes of one wave), rounded
+// outward to binary32, for frt_jit_tile (frt_jit_rt.hpp beam_box32); a tile without hits gets an empty box
+__device__ __forceinline__ void tile_box(int64_t node, int64_t n, bool hit, const double* op, float* __restrict__ tbox,
+                                         int tile_log2) {
+    float lo[3], hi[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = hit ? __double2float_rd(op[a]) : __builtin_huge_valf();
+        hi[a] = hit ? __double2float_ru(op[a]) : -__builtin_huge_valf();
+    }
+    for (int off = 1; off < (1 << tile_log2); off <<= 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], __shfl_xor(lo[a], off, 64));
+            hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off, 64));
+        }
+    }
+    if (node < n && (node & ((1 << tile_log2) - 1)) == 0) {
+        float* b = tbox + 6 * (node >> tile_log2);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            b[a] = lo[a];
+            b[a + 3] = hi[a];
+        }
+    }
+}
+
+template <bool kPat>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPat ? 1 : FRT_PREPARE_WAVES, 8)))
+k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const HitRec* __restrict__ hits,
+          NodeCols rec, ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q, unsigned long long* counters,
+          unsigned* err, float* __restrict__ tbox, int tile_log2) {
+    const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double op[3] = {0.0, 0.0, 0.0};
+    bool hit = false;
+    if (node < n) hit = prepare_node<kPat>(S, B, q, n, hits, rec, heads, next_q, counters, err, node, op);
+    if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2);
 }
 
 // one lane per (node, light sample j); lanes of a node are consecutive
@@ -1465,7 +1504,8 @@ __global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, NodeCols rec, i
 // host side: scene upload, buffer management, frame driver, C ABI
 // ======================================================================
 
-constexpr size_t kJitStatWords = 64 * 32 + 2 * 1024 + 2 * 2048;  // per-launch lines, node sites, beam sites
+// per-launch lines, node sites, beam sites; the tile kernel's beam sites at 1024 + 6144 + 2048
+constexpr size_t kJitStatWords = 16384;
 
 struct frt_scene_handle {
     int device = 0;
@@ -1480,6 +1520,14 @@ struct frt_scene_handle {
     // scene-specialised shadow kernel (frt_jit.hip); nullptr: the generic k_shadow runs
     void* jit_shadow = nullptr;
     void* jit_beam = nullptr;          // its pair kernel (frt_jit_beam)
+    void* jit_tile = nullptr;          // tile pair kernel (frt_jit_tile) and its listed tiles' node pairs
+    void* jit_list = nullptr;          //   (frt_jit_beam_list); null: frt_jit_beam decides every pair
+    int tile = 0;                      // path nodes per tile (frt_jit_tile_size), 0 without the tile kernels
+    float* tbox = nullptr;             // the level's tile boxes (k_prepare): 6 floats per tile
+    int64_t tbox_cap = 0;
+    uint32_t* tlist = nullptr;         // undecided (tile, light part) pairs, kMixSegs segments
+    int64_t tlist_cap = 0;
+    uint64_t tile_pairs = 0, tile_mixed = 0, node_pairs = 0, node_mixed = 0;  // this frame's pair-kernel counts
     bool jit_beam_on = true;           // FRT_JIT_BEAM=0: every pair is walked ray by ray (A/B)
     const int32_t* light_psamp = nullptr;  // the parts' samples (frt_jit_light_parts), -1 padded
     const float* light_aabb = nullptr; // per light, per cache row: the points' box (binary32, outward)
@@ -1791,12 +1839,15 @@ static std::vector<int> mesh_roots(const frt_scene* sc) {
     return roots;
 }
 
-// the BVHs of the mesh roots (host; one thread per mesh)
+// the BVHs of the mesh roots (host; a pool of at most 16 threads takes the meshes one by one)
 static std::vector<MeshBuild> mesh_build(const frt_scene* sc, const std::vector<int>& roots) {
     std::vector<MeshBuild> mb(roots.size());
     std::vector<std::thread> pool;
-    for (size_t m = 0; m < roots.size(); ++m)
-        pool.emplace_back([&, m]() {
+    std::atomic<size_t> next{0};
+    const size_t nthreads = std::min<size_t>(roots.size(), 16);
+    for (size_t t = 0; t < nthreads; ++t)
+        pool.emplace_back([&]() {
+          for (size_t m; (m = next.fetch_add(1)) < roots.size();) {
             const int g = roots[m];
             MeshBuild& B = mb[m];
             for (int j = g + 1; j < sc->nodes[g].skip; ++j) {
@@ -1814,10 +1865,13 @@ static std::vector<MeshBuild> mesh_build(const frt_scene* sc, const std::vector<
                 B.tris.push_back(t);
             }
             B.build(0, (int)B.tris.size(), 1);
+          }
         });
     for (auto& t : pool) t.join();
     return mb;
 }
+
+constexpr int kMeshStackMax = 32;
 
 // the scene's meshes: marks each root in wn (op = mesh index + 1), builds and uploads their BVHs;
 // S.meshes / num_meshes / mesh_stack
@@ -1848,7 +1902,10 @@ static int build_meshes(frt_scene_handle* h, const frt_scene* sc, std::vector<fr
     S.meshes = upload(h, desc.data(), desc.size(), rc);
     if (rc) return -1;
     S.num_meshes = (int32_t)roots.size();
-    S.mesh_stack = depth + 1;
+    // the per-lane LDS stack of the mesh searches (4 * kTraceBlock bytes per entry in every traversal block):
+    // capped, a search whose stack would overflow falls back to the group walk for its lane (mesh_closest /
+    // mesh_first), so a degenerate BVH costs speed, never the upload
+    S.mesh_stack = std::min(depth + 1, kMeshStackMax);
     return 0;
 }
 
@@ -2185,7 +2242,23 @@ int64_t frt_math_selftest(int64_t n, uint64_t seed) {
 
 const char* frt_last_error(void) { return g_last_error.c_str(); }
 
+// this thread's last frt_scene_upload, in ms (frt_upload_phases)
+static thread_local double t_upload_phases[8];
+
+int frt_upload_phases(double* out, int n) {
+    for (int i = 0; i < n && i < 8; ++i) out[i] = t_upload_phases[i];
+    return 8;
+}
+
 int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
+    const auto up0 = std::chrono::steady_clock::now();
+    auto up_last = up0;
+    auto phase = [&](int i) {  // the time since the previous mark into phase i
+        const auto t = std::chrono::steady_clock::now();
+        t_upload_phases[i] += std::chrono::duration<double, std::milli>(t - up_last).count();
+        up_last = t;
+    };
+    for (double& x : t_upload_phases) x = 0.0;
     if (sc == nullptr || out == nullptr) return fail("frt_scene_upload: null argument");
     if (sc->abi_version != FRT_ABI_VERSION) return fail("frt_scene_upload: ABI version mismatch");
     int ndev = frt_device_count();
@@ -2196,6 +2269,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     h->device = device;
     frt::DevScene& S = h->S;
     int rc = 0;
+    phase(0);
     S.nodes = upload(h, sc->nodes, (size_t)sc->num_nodes, rc);
     S.roots = upload(h, sc->roots, (size_t)sc->num_roots, rc);
     S.xforms = upload(h, sc->xforms, (size_t)sc->num_xforms * 16, rc);
@@ -2220,6 +2294,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         frt_scene_release(h);
         return -1;
     }
+    phase(1);
     {
         std::vector<frt::WalkNode> wn;
         build_walk_nodes(sc, wn);
@@ -2231,12 +2306,26 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         const char* jit_env = std::getenv("FRT_JIT");
         if (rc == 0 && sc->config.include_direct && !(jit_env && std::strcmp(jit_env, "0") == 0)) {
             std::string why, log;
+            phase(2);
             const std::string src = frt_jit_shadow_source(wn.data(), sc->num_nodes, sc->roots, sc->num_roots, sc->lights, sc->num_lights, why);
-            if (!src.empty() && frt_jit_compile(src, h->device, &h->jit_shadow, &h->jit_beam, log) != 0) {
+            phase(3);
+            FrtJitFns fns;
+            if (!src.empty() && frt_jit_compile(src, h->device, fns, log) != 0) {
                 why = "hiprtc: " + log.substr(0, 2000);
-                h->jit_shadow = nullptr;
-                h->jit_beam = nullptr;
+                fns = FrtJitFns{};
             }
+            if (!src.empty()) {
+                double ob = 0.0, ld = 0.0;
+                frt_jit_last_phases(&ob, &ld);
+                t_upload_phases[4] += ob;
+                t_upload_phases[5] += ld;
+                up_last = std::chrono::steady_clock::now();
+            }
+            h->jit_shadow = fns.shadow;
+            h->jit_beam = fns.beam;
+            h->jit_tile = fns.tile;
+            h->jit_list = fns.list;
+            h->tile = fns.tile && fns.list ? frt_jit_tile_size() : 0;
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
                 void* p = nullptr;
@@ -2394,6 +2483,8 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     }
     h->levels.resize((size_t)std::max(1, sc->config.path_length + 2));
     *out = h;
+    phase(6);
+    t_upload_phases[7] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - up0).count();
     return 0;
 }
 
@@ -2403,13 +2494,18 @@ void frt_scene_release(frt_scene_handle* h) {
     if (h->jit_stats) {
         std::vector<unsigned long long> c(kJitStatWords);
         if (hipMemcpy(c.data(), h->jit_stats, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
-            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0;
+            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0, tpairs = 0, tmixed = 0;
             for (int j = 0; j < 64; ++j) {
                 live += c[32 * j];
                 amb += c[32 * j + 1];
                 pairs += c[32 * j + 2];
                 mixed += c[32 * j + 3];
+                tpairs += c[32 * j + 4];
+                tmixed += c[32 * j + 5];
             }
+            if (tpairs)
+                std::fprintf(stderr, "frt jit stats: tile pair kernel (%d nodes per tile): live tile pairs %llu, mixed %llu (%.2f%%)\n",
+                             h->tile, tpairs, tmixed, 100.0 * (double)tmixed / (double)tpairs);
             std::fprintf(stderr, "frt jit stats: pair kernel: live pairs %llu, mixed %llu (%.2f%%)\n", pairs, mixed,
                          pairs ? 100.0 * (double)mixed / (double)pairs : 0.0);
             std::fprintf(stderr, "frt jit stats: live shadow lanes %llu, re-walked in binary64 %llu (%.4f%%)\n", live, amb,
@@ -2424,6 +2520,10 @@ void frt_scene_release(frt_scene_handle* h) {
                 if (c[3072 + 2 * k + 1])
                     std::fprintf(stderr, "frt jit stats: beam site %d: %llu waves, %llu lanes\n", k, c[3072 + 2 * k],
                                  c[3072 + 2 * k + 1]);
+            for (int k = 0; k < 2048; ++k)  // the tile kernel's
+                if (c[9216 + 2 * k + 1])
+                    std::fprintf(stderr, "frt jit stats: tile beam site %d: %llu waves, %llu lanes\n", k, c[9216 + 2 * k],
+                                 c[9216 + 2 * k + 1]);
         }
     }
     for (void* p : h->owned) hip_ignore(hipFree(p));
@@ -2459,6 +2559,9 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->counters));
     hip_ignore(hipFree(h->shade_lit));
     hip_ignore(hipFree(h->shade_lcount));
+    hip_ignore(hipFree(h->mixed));
+    hip_ignore(hipFree(h->tlist));
+    hip_ignore(hipFree(h->tbox));
     hip_ignore(hipFree(h->err));
     for (hipEvent_t e : h->ev_pool) hip_ignore(hipEventDestroy(e));
     if (h->ev[0]) hip_ignore(hipEventDestroy(h->ev[0]));
@@ -2598,57 +2701,148 @@ static void launch_shadow_redo_f(frt_scene_handle* h, const frt::Batch& B, const
                        h->j_light, h->j_point, h->samples_per_node, counts, h->err, h->redo, h->redo_count, h->redo_cap);
 }
 
-static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts) {
+// the block table of a segmented list (jit::SegTable) whose entries take lpe lanes each: returns the blocks,
+// `total` the entries (a segment past its capacity keeps its capacity: the error flag is set)
+static uint64_t seg_table(const std::vector<unsigned>& host_mcount, uint32_t segcap, uint64_t lpe,
+                          frt::jit::SegTable& seg, uint64_t& total) {
+    uint64_t nblk = 0;
+    total = 0;
+    for (int j = 0; j < frt::jit::kMixSegs; ++j) {
+        const uint64_t c = std::min<uint64_t>(host_mcount[(size_t)j * frt::jit::kMixLine], segcap);
+        seg.bstart[j] = (uint32_t)nblk;
+        seg.count[j] = (uint32_t)c;
+        total += c;
+        nblk += (c * lpe + frt::kTraceBlock - 1) / frt::kTraceBlock;
+    }
+    seg.bstart[frt::jit::kMixSegs] = (uint32_t)nblk;
+    return nblk;
+}
+
+// (node0: the first node's index in the level, for its tile box)
+static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::ShadowHead* rec, int64_t n, int32_t* counts,
+                          int64_t node0 = 0) {
     if (h->jit_shadow) {
-        // scene-specialised kernels: frt_jit_beam decides whole (node, light) pairs, frt_jit_shadow walks
-        // the rays of the mixed ones (32-bit lane index: at most 2^31 lanes per launch), then the
-        // generic walk takes the lanes handed back (non-finite rays, usually none)
+        // scene-specialised kernels: the pair kernels decide whole (node, light part) pairs — frt_jit_tile
+        // first for runs of tile consecutive nodes at once, frt_jit_beam_list for the nodes of the tile pairs
+        // it cannot decide (or frt_jit_beam for every pair) — and frt_jit_shadow walks the rays of the pairs
+        // left (32-bit lane index: at most 2^31 lanes per launch), then the generic walk takes the lanes
+        // handed back (non-finite rays, usually none)
         using frt::jit::kMixLine;
         using frt::jit::kMixSegs;
         int64_t NP = 0;  // parts of frt_jit_part_size() samples per path node (frt_jit_beam)
         for (const auto& L : h->host_lights) NP += std::max(1, (L.num_samples + frt_jit_part_size() - 1) / frt_jit_part_size());
         // the pair kernel's lane index is 32-bit: batches of more than 2^31 - 1 (node, part) pairs run
         // as node ranges (the shadow kernels read a node's ShadowHead and write its counts only, so a
-        // range is the same pass over rec + off and counts + off * lights)
+        // range is the same pass over rec + off and counts + off * lights; ranges start at tile boundaries)
         // (FRT_JIT_MAX_PAIRS lowers the limit: the tests split small batches this way)
         const char* mp_env = std::getenv("FRT_JIT_MAX_PAIRS");
         const long long mp = mp_env ? std::atoll(mp_env) : 0;
         const int64_t kMaxPairs = mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : (int64_t)((1ll << 31) - 1);
         if (n * NP > kMaxPairs) {
-            const int64_t per = std::max<int64_t>(1, kMaxPairs / NP);
+            int64_t per = std::max<int64_t>(1, kMaxPairs / NP);
+            if (h->tile > 0) per = std::max<int64_t>(h->tile, per / h->tile * h->tile);
             for (int64_t off = 0; off < n; off += per)
-                launch_shadow(h, B, rec + off, std::min(per, n - off), counts + off * h->S.num_lights);
+                launch_shadow(h, B, rec + off, std::min(per, n - off), counts + off * h->S.num_lights, node0 + off);
             return;
         }
         const int64_t npairs = n * NP;
-        const int64_t nblocks = (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
-        uint32_t segcap = h->jit_beam_on ? (uint32_t)(((nblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock)
-                                         : (uint32_t)std::max<int64_t>(1, npairs);
-        // pairs, then their resume values (frt_jit_rt.hpp mix_append)
-        if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
-            (void)hipGetLastError();
-            h->jit_shadow = nullptr;
-            launch_shadow(h, B, rec, n, counts);
-            return;
-        }
+        const bool tiled = h->jit_beam_on && h->tile > 0 && h->jit_tile && h->jit_list && h->tbox;
+        uint32_t nn = (uint32_t)n;
+        uint32_t segcap = 0;
         uint64_t total_mixed = 0;
-        hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
         if (h->jit_beam_on) {
-            uint32_t np = (uint32_t)npairs;
-            void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap,
-                             &h->err, &h->jit_stats};
-            hipError_t le;
+            frt::jit::SegTable tseg{};
+            uint32_t tsegcap = 0;
+            uint64_t list_blocks = 0, listed = 0;
+            int tl = 0;
+            while ((1 << tl) < h->tile) ++tl;
+            if (tiled) {
+                const int64_t ntiles = (n + h->tile - 1) >> tl;
+                uint32_t ntp = (uint32_t)(ntiles * NP);
+                const int64_t tblocks = (ntiles * NP + frt::kTraceBlock - 1) / frt::kTraceBlock;
+                tsegcap = (uint32_t)std::max<int64_t>(frt::kTraceBlock, ((tblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
+                if (grow(&h->tlist, h->tlist_cap, 2 * (int64_t)tsegcap * kMixSegs)) {  // (out of memory): the generic walk
+                    (void)hipGetLastError();
+                    h->jit_shadow = nullptr;
+                    launch_shadow(h, B, rec, n, counts, node0);
+                    return;
+                }
+                hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
+                const float* tb = h->tbox + 6 * (node0 >> tl);
+                const uint32_t* no_list = nullptr;
+                uint32_t zero = 0;
+                void* targs[] = {&h->S, (void*)&B, (void*)&rec, &ntp, &nn, (void*)&tb, (void*)&no_list, &tseg, &zero, &zero,
+                                 &h->light_aabb, &counts, &h->tlist, &h->mcount, &tsegcap, &h->err, &h->jit_stats};
+                hipError_t le;
+                {
+                    KTimer tt(h, h->cur_st, 12);
+                    le = hipModuleLaunchKernel((hipFunction_t)h->jit_tile, grid_for(ntiles * NP, frt::kTraceBlock), 1, 1,
+                                               frt::kTraceBlock, 1, 1, 0, h->stream, targs, nullptr);
+                }
+                if (le != hipSuccess) {
+                    std::fprintf(stderr, "frt: scene-specialised tile kernel launch failed (%s); pairs per node\n",
+                                 hipGetErrorString(le));
+                    (void)hipGetLastError();
+                    h->tile = 0;
+                    launch_shadow(h, B, rec, n, counts, node0);
+                    return;
+                }
+                if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                                   hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                    hipStreamSynchronize(h->stream) != hipSuccess)
+                    return;
+                list_blocks = seg_table(h->host_mcount, tsegcap, (uint64_t)h->tile, tseg, listed);
+                h->tile_pairs += ntp;
+                h->tile_mixed += listed;
+            }
+            // the mixed list of the node pairs: per segment, every lane of the blocks that append to it
+            const int64_t pblocks = tiled ? (int64_t)list_blocks : (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
+            segcap = (uint32_t)std::max<int64_t>(frt::kTraceBlock, ((pblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
+            // pairs, then their resume values (frt_jit_rt.hpp mix_append)
+            if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
+                (void)hipGetLastError();
+                h->jit_shadow = nullptr;
+                hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                launch_shadow(h, B, rec, n, counts, node0);
+                return;
+            }
+            hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
+            hipError_t le = hipSuccess;
             {
                 KTimer tb(h, h->cur_st, 8);
-                le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1, 1,
-                                           frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
+                if (tiled) {
+                    const uint64_t max_blocks = ((1ull << 31) - 1) / frt::kTraceBlock;
+                    const float* no_box = nullptr;
+                    uint32_t zero = 0;
+                    for (uint64_t b0 = 0; b0 < list_blocks && le == hipSuccess; b0 += max_blocks) {
+                        uint32_t b0u = (uint32_t)b0;
+                        void* largs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&no_box, &h->tlist, &tseg, &b0u,
+                                         &tsegcap, &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap, &h->err,
+                                         &h->jit_stats};
+                        le = hipModuleLaunchKernel((hipFunction_t)h->jit_list, (unsigned)std::min(max_blocks, list_blocks - b0), 1, 1,
+                                                   frt::kTraceBlock, 1, 1, 0, h->stream, largs, nullptr);
+                    }
+                    h->node_pairs += listed * (uint64_t)h->tile;
+                } else {
+                    uint32_t np = (uint32_t)npairs;
+                    const float* no_box = nullptr;
+                    const uint32_t* no_list = nullptr;
+                    frt::jit::SegTable no_seg{};
+                    uint32_t zero = 0;
+                    void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &nn, (void*)&no_box, (void*)&no_list, &no_seg, &zero, &zero,
+                                     &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap, &h->err, &h->jit_stats};
+                    le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1, 1,
+                                               frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
+                    h->node_pairs += (uint64_t)npairs;
+                }
             }
             if (le != hipSuccess) {
                 std::fprintf(stderr, "frt: scene-specialised pair kernel launch failed (%s); every pair per ray\n",
                              hipGetErrorString(le));
                 (void)hipGetLastError();
                 h->jit_beam_on = false;
-                launch_shadow(h, B, rec, n, counts);
+                hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                launch_shadow(h, B, rec, n, counts, node0);
                 return;
             }
             if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
@@ -2656,7 +2850,15 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 hipStreamSynchronize(h->stream) != hipSuccess)
                 return;
             for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
+            h->node_mixed += total_mixed;
         } else {
+            segcap = (uint32_t)std::max<int64_t>(1, npairs);
+            if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
+                (void)hipGetLastError();
+                h->jit_shadow = nullptr;
+                launch_shadow(h, B, rec, n, counts, node0);
+                return;
+            }
             total_mixed = (uint64_t)npairs;  // every pair, in order (frt_jit_shadow's all_pairs)
         }
         uint32_t all_pairs = h->jit_beam_on ? 0u : 1u;
@@ -3270,6 +3472,7 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
     h->cur_st = st;
     h->rays_walked = 0;
     h->pairs_walked = 0;
+    h->tile_pairs = h->tile_mixed = h->node_pairs = h->node_mixed = 0;
     const int rc = render_frame(h, P, dev_out, st);
     if (rc) h->gi.built = false;
     return rc;
@@ -3369,9 +3572,15 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             }
             {
                 KTimer t(h, st, 6);
+                // tile boxes for frt_jit_tile (scene-specialised shadow kernels with single-row lights)
+                const bool tiles = h->tile > 0 && h->jit_shadow && h->jit_beam_on && h->S.cfg.include_direct &&
+                                   h->samples_per_node > 0;
+                int tl = 0;
+                while (tiles && (1 << tl) < h->tile) ++tl;
+                if (tiles && grow(&h->tbox, h->tbox_cap, 6 * ((n >> tl) + 1))) return -1;
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
                                    dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
-                                   L.rec, L.head, N.q, h->counters, h->err);
+                                   L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl);
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.include_direct && h->samples_per_node > 0) {
@@ -3508,6 +3717,10 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->errors = err;
         st->shadow_jit = h->jit_shadow != nullptr ? 1 : 0;
         st->shadow_rays_walked = h->jit_shadow != nullptr ? h->rays_walked : st->shadow_rays;
+        st->shadow_tile_pairs = h->tile_pairs;
+        st->shadow_tile_mixed = h->tile_mixed;
+        st->shadow_pairs = h->node_pairs;
+        st->shadow_pairs_mixed = h->node_mixed;
         collect_timings(h, st);
     }
 #if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)

@@ -14,6 +14,9 @@ struct frt_light;
 // the pair kernel (frt_jit_beam) decides a light's samples in parts of this many consecutive samples
 // (FRT_JIT_PART overrides the default, for A/B runs)
 int frt_jit_part_size();
+// the tile pair kernel (frt_jit_tile) decides runs of this many consecutive path nodes at once (a power of two
+// up to 64; 0: off; FRT_JIT_TILE overrides the default 8)
+int frt_jit_tile_size();
 // the parts (frt_jit.hip): spatially compact groups of the light's samples; returns the part count
 int frt_jit_light_parts(const frt_light& L, const double* light_points, int PS, std::vector<int32_t>& order);
 
@@ -22,9 +25,19 @@ int frt_jit_light_parts(const frt_light& L, const double* light_points, int PS, 
 std::string frt_jit_shadow_source(const frt::WalkNode* wn, int num_nodes, const int32_t* roots, int num_roots,
                                   const frt_light* lights, int num_lights, std::string& why);
 
-// compile with hiprtc for `device` (cached per device and source); 0 on success, *fn = the per-ray
-// kernel frt_jit_shadow, *fn_beam = the pair kernel frt_jit_beam (hipFunction_t)
-int frt_jit_compile(const std::string& src, int device, void** fn, void** fn_beam, std::string& log);
+// the kernels of a scene's module (hipFunction_t; tile / list are null when the source has none)
+struct FrtJitFns {
+    void* shadow = nullptr;  // frt_jit_shadow: per ray
+    void* beam = nullptr;    // frt_jit_beam: every (node, part) pair
+    void* tile = nullptr;    // frt_jit_tile: every (tile, part) pair
+    void* list = nullptr;    // frt_jit_beam_list: the nodes of the listed tile pairs
+};
+// compile with hiprtc for `device` (cached per device and source); 0 on success
+int frt_jit_compile(const std::string& src, int device, FrtJitFns& fns, std::string& log);
+
+// this thread's last frt_jit_compile: ms to obtain the code object (0 when the process had it; a disk
+// read or a hiprtc compile otherwise) and to load it into the device's module
+void frt_jit_last_phases(double* obtain_ms, double* load_ms);
 
 // compile only (no device needed): 0 on success
 int frt_jit_compile_only(const std::string& src, const std::string& arch, std::string& log);

@@ -165,6 +165,9 @@ struct Node32 {
     int casts;
 };
 
+__device__ __forceinline__ float o_lo(const World32& w, int a) { return w.o[a]; }
+__device__ __forceinline__ float o_hi(const World32& w, int a) { return w.o[a]; }
+
 __device__ __forceinline__ void world32_finish(World32& w) {
     w.omax = fmaxf(fmaxf(fabsf(w.o[0]), fabsf(w.o[1])), fabsf(w.o[2]));
 #pragma unroll
@@ -449,6 +452,77 @@ __device__ __forceinline__ void beam32(const double* op, const float* pl, const 
     w.Dnmin = sqrtf(m2) * (1.0f - 8.0f * kU);
 }
 
+// ---- tiles: the beams of a run of T consecutive path nodes at once ----
+// The rays of a (tile, light part) beam start anywhere in the box [olo, ohi] of the tile's over_points
+// (binary64, rounded outward to binary32) and end anywhere in the part's box. D = p - o then lies in
+// [pl - ohi, ph - olo] and a slab numerator N = B - o_a in [B - ohi_a, B - olo_a]; the beam functions
+// below take both ends where Beam32 has one origin (kBox), so every decision they take holds for every
+// ray from every origin of the tile. s = t / |D| keeps its meaning ray by ray, DIST = 1 as before.
+struct BeamBox32 {
+    float olo[3], ohi[3], omax;
+    float pl[3], ph[3];     // the light part's box
+    float iDc[3][4];        // rcp of p - o at the corners (pl - olo, ph - olo, pl - ohi, ph - ohi), per axis
+    float Dlo[3], Dhi[3];
+    float ilo[3], ihi[3];
+    float im[3];
+    float Dmin[3];
+    float M[3];
+    float Dn, Dnmin;
+    bool sgn[3];
+};
+
+// the ends of the origin along axis a (one point for Beam32)
+__device__ __forceinline__ float o_lo(const Beam32& w, int a) { return w.o[a]; }
+__device__ __forceinline__ float o_hi(const Beam32& w, int a) { return w.o[a]; }
+__device__ __forceinline__ float o_lo(const BeamBox32& w, int a) { return w.olo[a]; }
+__device__ __forceinline__ float o_hi(const BeamBox32& w, int a) { return w.ohi[a]; }
+template <typename BW>
+struct BeamKind {
+    static constexpr bool kBox = false;
+};
+template <>
+struct BeamKind<BeamBox32> {
+    static constexpr bool kBox = true;
+};
+
+// the beam of a tile's origin box tb = {olo[3], ohi[3]} (binary32, rounded outward; olo > ohi: no live
+// node) and a light row's part box [pl, ph]; false: no ray
+__device__ __forceinline__ bool beam_box32(const float* tb, const float* pl, const float* ph, BeamBox32& w) {
+    float n2 = 0.0f, m2 = 0.0f;
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w.olo[a] = tb[a];
+        w.ohi[a] = tb[a + 3];
+        ok = ok && w.olo[a] <= w.ohi[a];
+        const float x0 = pl[a] - w.ohi[a], x1 = ph[a] - w.olo[a];
+        const float om = fmaxf(fabsf(w.olo[a]), fabsf(w.ohi[a]));
+        const float eD = 2.0f * kU * (om + fmaxf(fabsf(x0), fabsf(x1)));
+        w.Dlo[a] = x0 - eD;
+        w.Dhi[a] = x1 + eD;
+        w.sgn[a] = w.Dlo[a] > 0.0f || w.Dhi[a] < 0.0f;
+        w.ilo[a] = __builtin_amdgcn_rcpf(w.Dlo[a]);
+        w.ihi[a] = __builtin_amdgcn_rcpf(w.Dhi[a]);
+        w.im[a] = fmaxf(fabsf(w.ilo[a]), fabsf(w.ihi[a])) * (1.0f + 3.0f * kU);
+        const float M = fmaxf(fabsf(w.Dlo[a]), fabsf(w.Dhi[a]));
+        w.Dmin[a] = w.sgn[a] ? fminf(fabsf(w.Dlo[a]), fabsf(w.Dhi[a])) : 0.0f;
+        w.M[a] = M;
+        n2 = fmaf(M, M, n2);
+        m2 = fmaf(w.Dmin[a], w.Dmin[a], m2);
+        w.pl[a] = pl[a];
+        w.ph[a] = ph[a];
+        w.iDc[a][0] = __builtin_amdgcn_rcpf(pl[a] - w.olo[a]);
+        w.iDc[a][1] = __builtin_amdgcn_rcpf(ph[a] - w.olo[a]);
+        w.iDc[a][2] = __builtin_amdgcn_rcpf(pl[a] - w.ohi[a]);
+        w.iDc[a][3] = __builtin_amdgcn_rcpf(ph[a] - w.ohi[a]);
+    }
+    w.omax = fmaxf(fmaxf(fmaxf(fabsf(w.olo[0]), fabsf(w.ohi[0])), fmaxf(fabsf(w.olo[1]), fabsf(w.ohi[1]))),
+                   fmaxf(fabsf(w.olo[2]), fabsf(w.ohi[2])));
+    w.Dn = sqrtf(n2) * (1.0f + 8.0f * kU);
+    w.Dnmin = sqrtf(m2) * (1.0f - 8.0f * kU);
+    return ok;
+}
+
 // the s intervals of a slab plane pair (B0, B1) on axis a: false when D_a may change sign or the
 // reference's EPSILON branch may apply to some ray
 // thr: the node's aathr_a (0: no EPSILON branch), bmax >= |B0|, |B1|, sig: the node's aasig
@@ -463,37 +537,50 @@ __device__ __forceinline__ void beam32(const double* op, const float* pl, const 
 //    towards it enters the slab at s >= snear = (distance to the near plane - rs) / (max |D_a| towards it);
 //    aa_slab turns that into a certain miss when another axis certainly enters at s >= 0 (the away rays:
 //    tmin >= 0 > tmax) and snear lies beyond every exit bound of the decided axes (the towards rays).
-template <bool kSig>
-__device__ __forceinline__ bool beam_axis_split(float thr, float bmax, float sig, const Beam32& w, int a, float B0,
+template <bool kSig, typename BW>
+__device__ __forceinline__ bool beam_axis_split(float thr, float bmax, float sig, const BW& w, int a, float B0,
                                                 float B1, float& snear) {
-    const float N0 = fminf(B0, B1) - w.o[a], N1 = fmaxf(B0, B1) - w.o[a];
-    const float eN = fmaf(1.01f * kU, bmax + fabsf(w.o[a]), kU * fmaxf(fabsf(N0), fabsf(N1)));
+    // numerators over the origins: N0 in [N0lo, N0hi] = [Bl - ohi, Bl - olo], N1 likewise (one value each for
+    // a point origin)
+    const float Bl = fminf(B0, B1), Bh = fmaxf(B0, B1);
+    const float N0lo = Bl - o_hi(w, a), N1hi = Bh - o_lo(w, a);
+    const float N0hi = BeamKind<BW>::kBox ? Bl - o_lo(w, a) : N0lo, N1lo = BeamKind<BW>::kBox ? Bh - o_hi(w, a) : N1hi;
+    const float om = BeamKind<BW>::kBox ? fmaxf(fabsf(o_lo(w, a)), fabsf(o_hi(w, a))) : fabsf(o_lo(w, a));
+    const float nm = BeamKind<BW>::kBox ? fmaxf(fmaxf(fabsf(N0lo), fabsf(N0hi)), fmaxf(fabsf(N1lo), fabsf(N1hi)))
+                                        : fmaxf(fabsf(N0lo), fabsf(N1hi));
+    const float eN = fmaf(1.01f * kU, bmax + om, kU * nm);
     const float rs = eN + (kSig ? 1.01f * sig * w.omax : 0.0f);
     const float ds = kSig ? 1.01f * sig * w.Dn : 0.0f;
     const float f = 1.0f - 8.0f * kU;
     // lower bounds by reciprocal (within 3u of the quotient, inside f), the denominators raised to 2^-100
     // at least (a larger denominator keeps a lower bound, and no ray moving towards it, 0, becomes a finite
     // bound in place of +inf)
-    if (N0 - rs > 0.0f) {  // below the slab: D_a > 0 moves towards it
-        snear = (N0 - rs) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(w.Dhi[a], 0.0f) + ds, 0x1p-100f)) * f;
+    if (N0lo - rs > 0.0f) {  // below the slab (every origin): D_a > 0 moves towards it
+        snear = (N0lo - rs) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(w.Dhi[a], 0.0f) + ds, 0x1p-100f)) * f;
         return snear > 0.0f;
     }
-    if (-N1 - rs > 0.0f) {  // above
-        snear = (-N1 - rs) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(-w.Dlo[a], 0.0f) + ds, 0x1p-100f)) * f;
+    if (-N1hi - rs > 0.0f) {  // above
+        snear = (-N1hi - rs) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(-w.Dlo[a], 0.0f) + ds, 0x1p-100f)) * f;
         return snear > 0.0f;
     }
     return false;
 }
 
-template <bool kSig>
-__device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, const Beam32& w, int a, float B0, float B1,
+template <bool kSig, typename BW>
+__device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, const BW& w, int a, float B0, float B1,
                                           Iv& mn, Iv& mx) {
     const bool ok = w.sgn[a] && w.Dmin[a] >= thr * w.Dn;
-    const float N0 = fminf(B0, B1) - w.o[a], N1 = fmaxf(B0, B1) - w.o[a];
-    const float eN = fmaf(1.01f * kU, bmax + fabsf(w.o[a]), kU * fmaxf(fabsf(N0), fabsf(N1)));
+    const float Bl = fminf(B0, B1), Bh = fmaxf(B0, B1);
+    const float N0lo = Bl - o_hi(w, a), N1hi = Bh - o_lo(w, a);
+    const float N0hi = BeamKind<BW>::kBox ? Bl - o_lo(w, a) : N0lo, N1lo = BeamKind<BW>::kBox ? Bh - o_hi(w, a) : N1hi;
+    const float om = BeamKind<BW>::kBox ? fmaxf(fabsf(o_lo(w, a)), fabsf(o_hi(w, a))) : fabsf(o_lo(w, a));
+    const float nm = BeamKind<BW>::kBox ? fmaxf(fmaxf(fabsf(N0lo), fabsf(N0hi)), fmaxf(fabsf(N1lo), fabsf(N1hi)))
+                                        : fmaxf(fabsf(N0lo), fabsf(N1hi));
+    const float eN = fmaf(1.01f * kU, bmax + om, kU * nm);
     if (!ok) {
+        // (every origin strictly inside the slab: the smallest distances to its two planes)
         const float rs = eN + (kSig ? 1.01f * sig * w.omax : 0.0f);
-        const float r0 = -N0 - rs, r1 = N1 - rs;
+        const float r0 = -N0hi - rs, r1 = N1lo - rs;
         const float ds = kSig ? 1.01f * sig * w.Dn : 0.0f;
         // lower bounds by reciprocal, as in beam_axis_split (no ray of a sign: a finite bound in place of +inf)
         const float iMp = __builtin_amdgcn_rcpf(fmaxf(fmaxf(w.Dhi[a], 0.0f) + ds, 0x1p-100f));
@@ -504,11 +591,34 @@ __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, cons
         mx = Iv{vmx, __builtin_huge_valf()};
         return r0 > 0.0f && r1 > 0.0f && vmx > 0.0f && vmn > 0.0f;  // (false for NaN)
     }
-    const float q00 = N0 * w.ilo[a], q01 = N0 * w.ihi[a], q10 = N1 * w.ilo[a], q11 = N1 * w.ihi[a];
-    const float qm = fmaxf(fmaxf(fabsf(q00), fabsf(q01)), fmaxf(fabsf(q10), fabsf(q11)));
+    float lo0, hi0, lo1, hi1, qm;
+    if constexpr (BeamKind<BW>::kBox) {
+        // s = (B - o) / (p - o) over o in [olo, ohi], p in [pl, ph]. Where N = B - o keeps its sign over the
+        // origins and the plane lies outside the part's extent (B - p keeps its sign), s is monotone in o and in
+        // p (ds/do = (B - p) / D^2, ds/dp = -N / D^2): its range is that of the four corners (o, p), each with
+        // its own D (the corners' D are the beam's own exact binary32 values, rounded once: inside the same
+        // error term). Elsewhere the quotient's range over the independent N and D intervals.
+        const float eB = 1.01f * kU * bmax;
+        auto range = [&](float B, float Nlo, float Nhi, float& lo, float& hi) {
+            const bool mono = (Nlo > eN || Nhi < -eN) && (B + eB < w.pl[a] || B - eB > w.ph[a]);
+            const float c0 = Nhi * (mono ? w.iDc[a][0] : w.ilo[a]), c1 = Nhi * (mono ? w.iDc[a][1] : w.ihi[a]);
+            const float c2 = Nlo * (mono ? w.iDc[a][2] : w.ilo[a]), c3 = Nlo * (mono ? w.iDc[a][3] : w.ihi[a]);
+            lo = fminf(fminf(c0, c1), fminf(c2, c3));
+            hi = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3));
+        };
+        range(Bl, N0lo, N0hi, lo0, hi0);
+        range(Bh, N1lo, N1hi, lo1, hi1);
+        qm = fmaxf(fmaxf(fabsf(lo0), fabsf(hi0)), fmaxf(fabsf(lo1), fabsf(hi1)));
+    } else {
+        const float q00 = N0lo * w.ilo[a], q01 = N0lo * w.ihi[a], q10 = N1hi * w.ilo[a], q11 = N1hi * w.ihi[a];
+        qm = fmaxf(fmaxf(fabsf(q00), fabsf(q01)), fmaxf(fabsf(q10), fabsf(q11)));
+        lo0 = fminf(q00, q01);
+        hi0 = fmaxf(q00, q01);
+        lo1 = fminf(q10, q11);
+        hi1 = fmaxf(q10, q11);
+    }
     float err = 1.02f * fmaf(4.0f * kU, qm, eN * w.im[a]);
     if (kSig) err = fmaf(sig * w.im[a], fmaf(qm, w.Dn, w.omax) * 1.01f, err);
-    const float lo0 = fminf(q00, q01), hi0 = fmaxf(q00, q01), lo1 = fminf(q10, q11), hi1 = fmaxf(q10, q11);
     mn = Iv{fminf(lo0, lo1) - err, fminf(hi0, hi1) + err};
     mx = Iv{fmaxf(lo0, lo1) - err, fmaxf(hi0, hi1) + err};
     return ok;
@@ -516,8 +626,8 @@ __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, cons
 
 // the three slabs [B0_a, B1_a] of a world box on the beam (beam_axis per axis, beam_axis_split's certain
 // misses); thr: the EPSILON thresholds, bmax >= |B|, sig: the permutation remnants (kSig)
-template <bool kSig>
-__device__ __forceinline__ bool beam_slabs(const float* thr, float bmax, float sig, const Beam32& w, const float* B0,
+template <bool kSig, typename BW>
+__device__ __forceinline__ bool beam_slabs(const float* thr, float bmax, float sig, const BW& w, const float* B0,
                                            const float* B1, Iv& tmin, Iv& tmax) {
     bool ok = true, split_ok = true, any_ok = false;
     float snear = 0.0f;  // max over the split axes
@@ -556,28 +666,37 @@ template <bool kSig>
 __device__ __forceinline__ bool aa_slab(const Node32& nd, const Beam32& w, Iv& tmin, Iv& tmax) {
     return beam_slabs<kSig>(nd.aathr, nd.aabmax, nd.aasig, w, nd.aab, nd.aab + 3, tmin, tmax);
 }
+template <bool kSig>
+__device__ __forceinline__ bool aa_slab(const Node32& nd, const BeamBox32& w, Iv& tmin, Iv& tmax) {
+    return beam_slabs<kSig>(nd.aathr, nd.aabmax, nd.aasig, w, nd.aab, nd.aab + 3, tmin, tmax);
+}
 
 // frames that are not axis-aligned take no beam decision (their pairs are mixed)
-__device__ __forceinline__ void frame32i(const Node32&, const Beam32&, F32& f) {
+__device__ __forceinline__ void frame32i_none(F32& f) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) f.o[a] = f.d[a] = 0.0f;
     f.eo = 0.0f;
     f.ed = __builtin_huge_valf();  // slab_iv: |d| - ed < EPSILON -> undecided
 }
+__device__ __forceinline__ void frame32i(const Node32&, const Beam32&, F32& f) { frame32i_none(f); }
+__device__ __forceinline__ void frame32i(const Node32&, const BeamBox32&, F32& f) { frame32i_none(f); }
 
 // "wholly behind": every ray's t = |D| s <= Dnmin s_hi < -1e-6 (1 + |t|) (walk()'s behind())
 __device__ __forceinline__ bool behind_all(const Iv& tmax, const World32&) {
     return tmax.hi < -1e-6f * (1.0f + fabsf(tmax.hi));
 }
-__device__ __forceinline__ bool behind_all(const Iv& tmax, const Beam32& w) {
-    const float T = w.Dnmin * tmax.hi * (1.0f - 4.0f * kU);
+__device__ __forceinline__ bool behind_all_beam(const Iv& tmax, float Dnmin) {
+    const float T = Dnmin * tmax.hi * (1.0f - 4.0f * kU);
     return tmax.hi < 0.0f && T < -1.01e-6f * (1.0f + fabsf(T));
 }
+__device__ __forceinline__ bool behind_all(const Iv& tmax, const Beam32& w) { return behind_all_beam(tmax, w.Dnmin); }
+__device__ __forceinline__ bool behind_all(const Iv& tmax, const BeamBox32& w) { return behind_all_beam(tmax, w.Dnmin); }
 
 // a round sphere whose box every ray of the beam misses: the box, centre~ -+ (R' + 2u (|C~| + R') +
 // 1e-6 R') with R' = nd.sph[3] >= R (1 + 1e-6), holds the ball of radius R (1 + 1e-6) around the true
 // centre, so each line passes the centre at more than that (sphere_miss32's margin argument)
-__device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w) {
+template <typename BW>
+__device__ __forceinline__ bool sphere_miss32_beam(const Node32& nd, const BW& w) {
     // (the line misses the box: a direction component of 0 keeps the line out of a slab its origin is outside)
     const float h = nd.sph[3] + fmaf(2.0f * kU, nd.sphc + nd.sph[3], 1e-6f * nd.sph[3]);
     const float thr[3] = {0.0f, 0.0f, 0.0f};
@@ -587,12 +706,14 @@ __device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w)
     for (int a = 0; a < 3; ++a) {
         B0[a] = nd.sph[a] - h;
         B1[a] = nd.sph[a] + h;
-        near = near && fabsf(w.o[a] - nd.sph[a]) < 1e4f * nd.sph[3];
+        near = near && fmaxf(fabsf(o_lo(w, a) - nd.sph[a]), fabsf(o_hi(w, a) - nd.sph[a])) < 1e4f * nd.sph[3];
     }
     Iv tmin, tmax;
     const bool ok = beam_slabs<false>(thr, nd.sphc + h, 0.0f, w, B0, B1, tmin, tmax);
     return ok && near && tmin.lo > tmax.hi && w.omax < 1e8f * nd.sph[3];
 }
+__device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w) { return sphere_miss32_beam(nd, w); }
+__device__ __forceinline__ bool sphere_miss32(const Node32& nd, const BeamBox32& w) { return sphere_miss32_beam(nd, w); }
 
 // a round sphere the beam may meet (a top-level leaf of the pair kernel's walk):
 //  1  every ray of the beam hits it with its first root in (0, distance): the walk stops there, blocked
@@ -609,34 +730,53 @@ __device__ __forceinline__ bool sphere_miss32(const Node32& nd, const Beam32& w)
 //    cone about v of half-angle asin(Rc / |v|), Rc = R' (1 - 1e-5) (1 - 1e-4) - 1.75 ea (the cone is
 //    convex: its 8 corners decide, with a 1e-4 relative slack over their binary32 dot products), so each
 //    line passes the true centre closer than R (1 - 1e-4): two roots, the first in (0, |a|], |a| < |D|.
-__device__ __forceinline__ int sphere_beam32(const Node32& nd, const Beam32& w) {
+// (o: the origin; h: for a tile, the largest distance of any origin of its box from o, else 0 — a line through
+// another origin O' parallel to one through o lies within h of it, and |C - O'| within h of |C - o|)
+__device__ __forceinline__ int sphere_beam32_at(const Node32& nd, const float* o, float omax, float h, const float* Dlo,
+                                                const float* Dhi, float Dnmin) {
     float v[3], vv = 0.0f, vm = 0.0f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        v[a] = nd.sph[a] - w.o[a];
+        v[a] = nd.sph[a] - o[a];
         vv = fmaf(v[a], v[a], vv);
         vm = fmaxf(vm, fabsf(v[a]));
     }
-    const float ea = 1.75f * fmaf(2.0f * kU, nd.sphc + nd.sph[3], kU * (w.omax + vm));
+    const float ea = 1.75f * fmaf(2.0f * kU, nd.sphc + nd.sph[3], kU * (omax + vm)) + h;
     const float vn = sqrtf(vv);
     const float Rp = nd.sph[3];
     const float near_hi = fmaf(vn, 1.0f + 4.0f * kU, ea);  // >= |a|
-    const float lim = w.Dnmin * (1.0f - 1e-5f);
-    const bool before = near_hi + Rp < lim && vm < 1e4f * Rp && w.omax < 1e8f * Rp;
+    const float lim = Dnmin * (1.0f - 1e-5f);
+    const bool before = near_hi + Rp < lim && vm + h < 1e4f * Rp && omax < 1e8f * Rp;
     if (!before) return 0;
     const float Rc = fmaf(Rp, (1.0f - 1e-5f) * (1.0f - 1e-4f), -ea);
     bool hit = fmaf(vn, 1.0f - 4.0f * kU, -ea) > 1.01f * Rp && near_hi < lim && Rc > 0.0f;
     const float k2 = (vv - Rc * Rc) * (1.0f + 1e-4f);  // |v|^2 cos^2 of the half-angle
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float d0 = (j & 1) ? w.Dhi[0] : w.Dlo[0];
-        const float d1 = (j & 2) ? w.Dhi[1] : w.Dlo[1];
-        const float d2 = (j & 4) ? w.Dhi[2] : w.Dlo[2];
+        const float d0 = (j & 1) ? Dhi[0] : Dlo[0];
+        const float d1 = (j & 2) ? Dhi[1] : Dlo[1];
+        const float d2 = (j & 4) ? Dhi[2] : Dlo[2];
         const float dv = fmaf(d0, v[0], fmaf(d1, v[1], d2 * v[2]));
         const float dd = fmaf(d0, d0, fmaf(d1, d1, d2 * d2));
         hit = hit && dv > 0.0f && dv * dv > dd * k2;
     }
     return hit ? 1 : 2;
+}
+__device__ __forceinline__ int sphere_beam32(const Node32& nd, const Beam32& w) {
+    return sphere_beam32_at(nd, w.o, w.omax, 0.0f, w.Dlo, w.Dhi, w.Dnmin);
+}
+// a tile's beam: from the centre of its origin box, h = the box's half diagonal (rounded up, with the centre's
+// rounding); the D box covers every origin already
+__device__ __forceinline__ int sphere_beam32(const Node32& nd, const BeamBox32& w) {
+    float o[3], h2 = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        o[a] = 0.5f * (w.olo[a] + w.ohi[a]);
+        const float e = fmaxf(w.ohi[a] - o[a], o[a] - w.olo[a]);
+        h2 = fmaf(e, e, h2);
+    }
+    const float h = sqrtf(h2) * (1.0f + 8.0f * kU) + 2.0f * kU * w.omax;
+    return sphere_beam32_at(nd, o, w.omax, h, w.Dlo, w.Dhi, w.Dnmin);
 }
 
 // the slab entries tmin / tmax as intervals; false when |d_a| may be below EPSILON
@@ -719,7 +859,7 @@ __device__ __forceinline__ bool inside_aa(const Node32& nd, const W& w) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float lo = fminf(nd.aab[a], nd.aab[a + 3]), hi = fmaxf(nd.aab[a], nd.aab[a + 3]);
-        in = in && w.o[a] - lo > m && hi - w.o[a] > m;
+        in = in && o_lo(w, a) - lo > m && hi - o_hi(w, a) > m;
     }
     return in;
 }
@@ -787,13 +927,14 @@ __device__ __forceinline__ void cube_top32(const Node32& nd, const W& w, const I
 // ray lies on the cube's surface (|t| <= the farthest corner's distance F from the origin; the EPSILON
 // branch moves it by < 1e-5 |t|), so any entry > 0 is also < |D|. The world box is the node's slab planes
 // (binary32, within u aabmax, remnants sigma (|o| + F)); o~ within u |o| per axis; 1.75 > sqrt(3).
-template <int kAa>
-__device__ __forceinline__ bool cube_before_light(const Node32& nd, const Beam32& w) {
+template <int kAa, typename BW>
+__device__ __forceinline__ bool cube_before_light(const Node32& nd, const BW& w) {
     if (kAa == 0) return false;
     float f2 = 0.0f;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float m = fmaxf(fabsf(nd.aab[a] - w.o[a]), fabsf(nd.aab[a + 3] - w.o[a]));
+    for (int a = 0; a < 3; ++a) {  // (over a tile's origin box: both of its ends)
+        float m = fmaxf(fabsf(nd.aab[a] - o_lo(w, a)), fabsf(nd.aab[a + 3] - o_lo(w, a)));
+        if (BeamKind<BW>::kBox) m = fmaxf(m, fmaxf(fabsf(nd.aab[a] - o_hi(w, a)), fabsf(nd.aab[a + 3] - o_hi(w, a))));
         f2 = fmaf(m, m, f2);
     }
     const float F = sqrtf(f2) * (1.0f + 8.0f * kU);
@@ -803,8 +944,8 @@ __device__ __forceinline__ bool cube_before_light(const Node32& nd, const Beam32
 
 // (pair kernel) cube_top32, but a cube the beam cannot decide that lies wholly before the light and casts
 // shadows can only stop the walk blocked or leave it going: the lane goes on marked ms (maybe blocked)
-template <int kAa>
-__device__ __forceinline__ void cube_top32_beam(const Node32& nd, const Beam32& w, const Iv& dist, bool act,
+template <int kAa, typename BW>
+__device__ __forceinline__ void cube_top32_beam(const Node32& nd, const BW& w, const Iv& dist, bool act,
                                                 bool& alive, int& result, bool& any_entry, bool& amb, bool& ms) {
     bool undecided = false;
     cube_top32<kAa>(nd, w, dist, act, alive, result, any_entry, undecided);

@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "frt_device.h"
 #include "frt_flatten.h"
@@ -178,6 +179,14 @@ render_devices(int *dev, int cap, char *err, size_t errlen)
     return n;
 }
 
+static double
+now_ms(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return 1e3 * (double)ts.tv_sec + 1e-6 * (double)ts.tv_nsec;
+}
+
 /* one device's share of the frame: upload, render rows k, k+N, k+2N, ..., release */
 typedef struct {
     const frt_scene *fs;
@@ -189,6 +198,7 @@ typedef struct {
     frt_frame_stats st;
     int rc;
     char err[512];
+    double upload_ms, upload_phases[8], render_ms, release_ms;
 } device_job;
 
 static void *
@@ -196,11 +206,15 @@ device_worker(void *arg)
 {
     device_job *j = (device_job *)arg;
     frt_scene_handle *h = NULL;
+    const double t0 = now_ms();
     j->rc = frt_scene_upload(j->fs, j->device, &h);
+    j->upload_ms = now_ms() - t0;
+    frt_upload_phases(j->upload_phases, 8);
     if (j->rc) {
         snprintf(j->err, sizeof(j->err), "device %d: upload: %s", j->device, frt_last_error());
         return NULL;
     }
+    const double t1 = now_ms();
     frt_frame_params p;
     memset(&p, 0, sizeof(p));
     p.row_begin = j->k;
@@ -208,11 +222,31 @@ device_worker(void *arg)
     p.row_stride = j->n;
     p.seed = j->seed;
     j->rc = frt_render_rows(h, &p, j->rows, j->want_stats ? &j->st : NULL);
+    j->render_ms = now_ms() - t1;
     if (j->rc) {
         snprintf(j->err, sizeof(j->err), "device %d: render: %s", j->device, frt_last_error());
     }
+    const double t2 = now_ms();
     frt_scene_release(h);
+    j->release_ms = now_ms() - t2;
     return NULL;
+}
+
+/* the phases of the last render_multi on this process, in ms (frt_render_multi_phases) */
+static double g_rm_phases[16];
+
+/*
+ * Diagnostics: the phases of the last render_multi, in ms: out[0] flatten, [1] upload (the slowest device),
+ * [2..9] that device's frt_upload_phases, [10] render of its rows incl. the copy to host memory (the slowest
+ * device), [11] placing the rows into the canvas, [12] release, [13] total. Writes min(n, 14); returns 14.
+ */
+int
+frt_render_multi_phases(double *out, int n)
+{
+    for (int i = 0; i < n && i < 14; ++i) {
+        out[i] = g_rm_phases[i];
+    }
+    return 14;
 }
 
 /*
@@ -227,6 +261,8 @@ device_worker(void *arg)
 Canvas
 render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
 {
+    const double rm0 = now_ms();
+    memset(g_rm_phases, 0, sizeof(g_rm_phases));
     const size_t width = cam != NULL ? cam->hsize : 1, height = cam != NULL ? cam->vsize : 1;
     Canvas c = canvas_alloc(width, height, false, NULL);
     memset(c->arr, 0, width * height * sizeof(Color));
@@ -234,7 +270,9 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     char err[512];
     frt_scene fs;
     g_render_error[0] = '\0';
-    if (host_flatten(cam, w, usteps, vsteps, jitter, &fs)) {
+    const int flat_rc = host_flatten(cam, w, usteps, vsteps, jitter, &fs);
+    g_rm_phases[0] = now_ms() - rm0;
+    if (flat_rc) {
         fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", g_host_error);
         snprintf(g_render_error, sizeof(g_render_error), "%s", g_host_error);
         return c;
@@ -298,6 +336,19 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
         }
     }
     if (!failed) {
+        int slow = 0;
+        for (int k = 0; k < n; ++k) {
+            if (jobs[k].upload_ms > jobs[slow].upload_ms) {
+                slow = k;
+            }
+            g_rm_phases[10] = jobs[k].render_ms > g_rm_phases[10] ? jobs[k].render_ms : g_rm_phases[10];
+            g_rm_phases[12] = jobs[k].release_ms > g_rm_phases[12] ? jobs[k].release_ms : g_rm_phases[12];
+        }
+        g_rm_phases[1] = jobs[slow].upload_ms;
+        memcpy(g_rm_phases + 2, jobs[slow].upload_phases, 8 * sizeof(double));
+    }
+    const double place0 = now_ms();
+    if (!failed) {
         for (int k = 0; k < n; ++k) {
             const device_job *j = &jobs[k];
             int64_t i = 0;
@@ -313,6 +364,7 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
                 total.render_ms = j->st.render_ms;
             }
         }
+        g_rm_phases[11] = now_ms() - place0;
         if (stats_path) {
             write_stats(stats_path, &total, cam, usteps, vsteps, n);
         }
@@ -326,6 +378,7 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     free(jobs);
     free(th);
     frt_flat_scene_free(&fs);
+    g_rm_phases[13] = now_ms() - rm0;
     return c;
 }
 

@@ -37,11 +37,13 @@ class FrameStats(ctypes.Structure):
                 ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double),
                 ("shadow_jit", ctypes.c_int32), ("photon_pass", ctypes.c_int32),
                 ("sub_ms", ctypes.c_double * 8), ("sub_launches", ctypes.c_uint64 * 8),
-                ("shadow_rays_walked", ctypes.c_uint64)]
+                ("shadow_rays_walked", ctypes.c_uint64), ("shadow_tile_pairs", ctypes.c_uint64),
+                ("shadow_tile_mixed", ctypes.c_uint64), ("shadow_pairs", ctypes.c_uint64),
+                ("shadow_pairs_mixed", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
-        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit"]
+        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
@@ -55,6 +57,8 @@ class FrameStats(ctypes.Structure):
             "sub_ms": {subs[i]: float(self.sub_ms[i]) for i in range(len(subs)) if self.sub_launches[i]},
             "sub_launches": {subs[i]: int(self.sub_launches[i]) for i in range(len(subs)) if self.sub_launches[i]},
             "shadow_rays_walked": int(self.shadow_rays_walked),
+            "shadow_tile_pairs": int(self.shadow_tile_pairs), "shadow_tile_mixed": int(self.shadow_tile_mixed),
+            "shadow_pairs": int(self.shadow_pairs), "shadow_pairs_mixed": int(self.shadow_pairs_mixed),
         }
 
 
@@ -231,6 +235,23 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
     if err:
         raise RuntimeError("frt: render_multi failed: " + err.decode(errors="replace"))
     return out
+
+
+RENDER_MULTI_PHASES = ("flatten", "upload", "upload.device_select", "upload.scene_buffers", "upload.walk_records_meshes",
+                       "upload.jit_source", "upload.jit_code_object", "upload.jit_module_load", "upload.rest",
+                       "upload.total", "render_rows_and_copy", "place_rows", "release", "total")
+
+
+def render_multi_phases() -> dict:
+    """The phases of this process's last render_multi in ms (host/frt_render.c frt_render_multi_phases):
+    flatten, the slowest device's upload and its sub-phases (frt_upload_phases), render incl. the copy to
+    host memory, placing the rows into the canvas, release, total."""
+    lib = host_lib()
+    lib.frt_render_multi_phases.restype = ctypes.c_int
+    lib.frt_render_multi_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    out = (ctypes.c_double * 14)()
+    lib.frt_render_multi_phases(out, 14)
+    return {k: round(float(v), 3) for k, v in zip(RENDER_MULTI_PHASES, out)}
 
 
 def cpu_share() -> int:

@@ -217,11 +217,17 @@ typedef struct frt_frame_stats {
     int32_t shadow_jit;           /* 1: the scene-specialised shadow kernel ran (frt_jit.hip), 0: the generic walk */
     int32_t photon_pass;          /* 1: this frame traced its photon maps (a new seed), 0: maps reused / no GI */
     /* kernels inside the slots above (HIP events around each launch on the engine stream):
-       0 frt_jit_beam (pair kernel), 1 frt_jit_shadow (per-ray kernel), 2 k_gather_est, 3 k_gather_hit */
+       0 frt_jit_beam / frt_jit_beam_list (node pair kernel), 1 frt_jit_shadow (per-ray kernel), 2 k_gather_est,
+       3 k_gather_hit, 4 frt_jit_tile (tile pair kernel) */
     double sub_ms[8];
     uint64_t sub_launches[8];
     uint64_t shadow_rays_walked;  /* shadow rays walked one by one; the rest of shadow_rays were resolved
                                      (exactly, for every ray) per (node, light part) by frt_jit_beam */
+    /* the scene-specialised pair kernels' work this frame (0 without them) */
+    uint64_t shadow_tile_pairs;   /* (tile of consecutive path nodes, light part) beams frt_jit_tile tested */
+    uint64_t shadow_tile_mixed;   /* of those, the ones it could not decide (their nodes go to frt_jit_beam_list) */
+    uint64_t shadow_pairs;        /* (path node, light part) beams tested by frt_jit_beam / frt_jit_beam_list */
+    uint64_t shadow_pairs_mixed;  /* of those, the ones whose rays frt_jit_shadow walked */
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */
@@ -270,6 +276,13 @@ int64_t frt_math_selftest(int64_t n, uint64_t seed);
  * $XDG_CACHE_HOME/frt_jit or ~/.cache/frt_jit; FRT_JIT_CACHE=0 turns it off), once per machine.
  * Writes min(n, 5) counters; returns 5. */
 int frt_jit_cache_stats(int64_t *out, int n);
+
+/* Diagnostics: the phases of this thread's last frt_scene_upload, in ms: out[0] device selection (the
+ * process's first HIP call initialises the runtime here), [1] scene buffers to HBM, [2] walk records and
+ * mesh BVHs, [3] the scene-specialised kernels' source, [4] their code object (0 when this process had it;
+ * an on-disk cache read or a hiprtc compile otherwise), [5] its load into the device's module, [6] the
+ * rest (light tables, work buffers, stream), [7] total. Writes min(n, 8); returns 8. */
+int frt_upload_phases(double *out, int n);
 
 /* Photon map entry points (parity tests; no scene needed).
  * frt_pm_balance replaces pm_balance (reference src/libs/photon_map/pm.c:329-494): the balanced

@@ -117,6 +117,25 @@ def test_gpu_matches_oracle_on_headline_rows(built):
     assert encode_band(gpu) == encode_band(cpu)
 
 
+def test_gpu_matches_oracle_on_headline_dense_band(built):
+    """32 consecutive rows of the headline frame across the window's penumbra on the floor and walls (rows
+    700-731: the rows where the shadow pass's pair decisions and the shading's per-point arithmetic vary most)
+    against the oracle: every channel within 1e-4 and the band's 16-bit PPM values identical — the count of
+    differing values is printed (0 required), so a drift of the shading's refined estimates that flips a
+    quantised value anywhere in the band fails here."""
+    import oracle
+    from fast_ray_tracer_amd.runtime import cpu_share, encode_ppm
+    gpu = renderer(HEADLINE).render(700, 732)
+    cpu = oracle.render(load_scene(HEADLINE), 700, 732, threads=cpu_share())
+    diff = np.abs(gpu - cpu)
+    pg = np.frombuffer(encode_ppm(gpu[:, :, :3]), dtype=np.uint8)
+    pc = np.frombuffer(encode_ppm(cpu[:, :, :3]), dtype=np.uint8)
+    flips = int((pg != pc).sum())
+    print(f"rows 700-731: max|d|={diff.max():.3e} mismatching channels={(diff > 0).mean():.4%} PPM bytes differing={flips}")
+    assert diff.max() <= TOL
+    assert flips == 0
+
+
 def encode_band(rgba):
     from fast_ray_tracer_amd.runtime import encode_ppm
     return hashlib.sha256(encode_ppm(rgba[:, :, :3])).hexdigest()
@@ -210,10 +229,21 @@ def test_jit_compiled_once_and_cached_on_disk(built, tmp_path):
     second = probe()
     print("second process", second)
     assert second["after_handles"]["compiles"] == 0 and second["after_render_multi"]["disk_hits"] == 1
-    # a cold render_multi in a new process: no compile (a gfx950 hiprtc compile of this kernel is ~0.9 s;
-    # the bound leaves room for the process's first module load, allocations and stream setup, which
-    # measured 130-210 ms on different boxes)
-    assert second["cold_ms"] <= second["warm_ms"] + 400.0, second
+    # a cold render_multi in a new process compiles nothing (the counters above); its wall time is printed for
+    # the record only (the process's first module load and allocations vary by box: bench.py reports the
+    # phases of a second process's render_multi, render_multi_phases_second_process)
+    print("second process: cold %.1f ms, warm %.1f ms" % (second["cold_ms"], second["warm_ms"]))
+    # a corrupt cached object (its payload checksum fails) is dropped and compiled again, and renders
+    co = [f for f in os.listdir(tmp_path / "co") if f.endswith(".co")]
+    assert len(co) == 1
+    path = tmp_path / "co" / co[0]
+    data = bytearray(open(path, "rb").read())
+    data[-100] ^= 0xFF
+    open(path, "wb").write(bytes(data))
+    third = probe()
+    print("third process (corrupt cache)", third)
+    assert third["after_render_multi"]["compiles"] == 1 and third["after_render_multi"]["disk_hits"] == 0
+    assert third["after_render_multi"]["disk_writes"] == 1
 
 
 def test_gpu_matches_oracle_on_cfg4_rows(built):
@@ -301,7 +331,7 @@ def test_gather_queue_equals_static_ranges(built):
 
 
 @pytest.mark.parametrize("name", ["bounding_boxes_800x1000_4x4", "bounding_boxes_100x125_4x4", "teapot_low_100",
-                                  "nave_120x150_4x4"])
+                                  "nave_120x150_4x4", "degenerate_mesh_48"])
 def test_mesh_search_equals_generic_walk(built, name):
     """Mesh subtrees (groups of triangles, frt_traverse.hpp MeshDesc) are searched per lane in a BVH of their
     own, closest hit and the shadow walk's first-in-pre-order entry alike; the answer must be the generic

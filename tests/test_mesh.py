@@ -18,7 +18,7 @@ SCENES = sorted(f[:-2] for f in os.listdir(os.path.join(GOLDEN, "scenes")) if f.
 # the scenes with meshes (groups of >= 64 triangles in trees over 512 nodes): meshes, triangles in them
 # (bounding_boxes: 6 dragons of 23 490 faces each, dragon.obj)
 MESHES = {"bounding_boxes_800x1000_4x4": (6, 140940), "bounding_boxes_100x125_4x4": (6, 140940),
-          "bounding_boxes_200x80": (6, 140940)}
+          "bounding_boxes_200x80": (6, 140940), "degenerate_mesh_48": (1, 600)}
 
 
 @pytest.mark.parametrize("name", SCENES)
@@ -33,6 +33,16 @@ def test_mesh_bvh_sound(built, name):
         # a binary tree over T triangles in leaves of <= 4: at least T/4 - 1 inner nodes, fewer than T
         assert st["triangles"] // 4 - st["meshes"] <= st["bvh_nodes"] < st["triangles"], st
         assert st["depth"] <= 64, st
+
+
+def test_degenerate_mesh_is_deeper_than_the_search_stack(built):
+    """The degenerate fixture (tests/golden/make_fixture_degenerate.py) builds a BVH deeper than the per-lane
+    search stack (frt_engine.hip kMeshStackMax = 32): the upload caps the stack instead of growing every
+    traversal block's LDS, and the searches fall back to the group walk where it is full (the GPU image
+    equals the plain walk's: test_gpu_parity.py test_mesh_search_equals_generic_walk)."""
+    from fast_ray_tracer_amd.runtime import mesh_check
+    bad, st = mesh_check(load_scene("degenerate_mesh_48"))
+    assert bad == 0 and st["depth"] > 32, st
 
 
 def test_mesh_switch_off(built, monkeypatch):
