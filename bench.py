@@ -234,14 +234,23 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
         rays_per_launch = (d.get("shadow_rays_walked") or 0) / nl
         roof["issue"] = {kname: issue_block(t, avg_ms, rays_per_launch, "rays")}
         roof["issue"][kname]["source"] = os.path.relpath(path, ROOT)
+    # the pair kernels: the node pairs (frt_jit_beam_list after the tile kernel, frt_jit_beam without it; one
+    # timer slot) and the tile pairs (frt_jit_tile)
     nb = d.get("sub_launches", {}).get("frt_jit_beam")
-    fb = latest_pmc("frt_jit_beam", workload)
+    tiled = bool(d.get("shadow_tile_pairs"))
+    bname = "frt_jit_beam_list" if tiled else "frt_jit_beam"
+    fb = latest_pmc(bname, workload)
     if nb and fb:
         bavg = d["sub_ms"]["frt_jit_beam"] / nb
         pairs_per_launch = (d.get("shadow_pairs") or 0) / nb
-        roof.setdefault("issue", {})["frt_jit_beam"] = dict(issue_block(fb[1], bavg, pairs_per_launch, "pairs"),
-                                                            avg_launch_ms=round(bavg, 4),
-                                                            source=os.path.relpath(fb[0], ROOT))
+        roof.setdefault("issue", {})[bname] = dict(issue_block(fb[1], bavg, pairs_per_launch, "pairs"),
+                                                   avg_launch_ms=round(bavg, 4), source=os.path.relpath(fb[0], ROOT))
+    nt = d.get("sub_launches", {}).get("frt_jit_tile")
+    ft = latest_pmc("frt_jit_tile", workload)
+    if nt and ft:
+        tavg = d["sub_ms"]["frt_jit_tile"] / nt
+        roof.setdefault("issue", {})["frt_jit_tile"] = dict(issue_block(ft[1], tavg, d["shadow_tile_pairs"] / nt, "tile_pairs"),
+                                                            avg_launch_ms=round(tavg, 4), source=os.path.relpath(ft[0], ROOT))
     return roof
 
 
@@ -542,7 +551,7 @@ def main():
             "sub_ms_per_frame": {k: round(v, 4) for k, v in d.get("sub_ms", {}).items()},
             "shadow_pass": {
                 "kernels_ms_per_frame": {k: round(v, 4) for k, v in d.get("sub_ms", {}).items()
-                                         if k in ("frt_jit_beam", "frt_jit_shadow")},
+                                         if k in ("frt_jit_beam", "frt_jit_shadow", "frt_jit_tile")},
                 "shadow_rays_per_frame": d["shadow_rays"],
                 "shadow_rays_walked_per_ray": d.get("shadow_rays_walked"),
                 "tile_pairs": d.get("shadow_tile_pairs"), "tile_pairs_mixed": d.get("shadow_tile_mixed"),
@@ -552,8 +561,10 @@ def main():
                 "rays_walked_frac": (round(d["shadow_rays_walked"] / d["shadow_rays"], 4)
                                      if d.get("shadow_rays") else None),
                 "note": "every shadow ray's occlusion is computed exactly (bit-identical to a per-ray walk, "
-                        "tests/test_jit.py); frt_jit_beam resolves whole (path node, light part) pairs by interval "
-                        "bounds over all their rays, frt_jit_shadow walks the rays of the pairs it cannot decide"},
+                        "tests/test_jit.py); frt_jit_tile resolves (tile of consecutive path nodes, light part) "
+                        "beams, frt_jit_beam (frt_jit_beam_list after the tile kernel; one timer) the (path node, "
+                        "light part) pairs of the tiles left, by interval bounds over all their rays; frt_jit_shadow "
+                        "walks the rays of the pairs left"},
             "roofline": roof,
         }
         out.update(rm)

@@ -27,6 +27,9 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1523,6 +1526,7 @@ struct frt_scene_handle {
     void* jit_tile = nullptr;          // tile pair kernel (frt_jit_tile) and its listed tiles' node pairs
     void* jit_list = nullptr;          //   (frt_jit_beam_list); null: frt_jit_beam decides every pair
     int tile = 0;                      // path nodes per tile (frt_jit_tile_size), 0 without the tile kernels
+    uint64_t scene_key = 0;            // hash of the flattened scene's content (shared photon maps)
     float* tbox = nullptr;             // the level's tile boxes (k_prepare): 6 floats per tile
     int64_t tbox_cap = 0;
     uint32_t* tlist = nullptr;         // undecided (tile, light part) pairs, kMixSegs segments
@@ -2242,8 +2246,16 @@ int64_t frt_math_selftest(int64_t n, uint64_t seed) {
 
 const char* frt_last_error(void) { return g_last_error.c_str(); }
 
+static std::atomic<long long> g_maps_stat[2];  // photon passes traced, photon passes shared (build_photon_maps)
+
 // this thread's last frt_scene_upload, in ms (frt_upload_phases)
 static thread_local double t_upload_phases[8];
+
+// process-wide photon passes: out[0] traced, out[1] taken from another device's trace (build_photon_maps)
+int frt_photon_pass_stats(int64_t* out, int n) {
+    for (int i = 0; i < n && i < 2; ++i) out[i] = g_maps_stat[i].load();
+    return 2;
+}
 
 int frt_upload_phases(double* out, int n) {
     for (int i = 0; i < n && i < 8; ++i) out[i] = t_upload_phases[i];
@@ -2269,6 +2281,28 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     h->device = device;
     frt::DevScene& S = h->S;
     int rc = 0;
+    {  // the scene's identity for the process-wide photon-map sharing (build_photon_maps)
+        uint64_t k = 0xcbf29ce484222325ull;
+        auto mix = [&](const void* p, size_t n) {
+            const unsigned char* c = (const unsigned char*)p;
+            for (size_t i = 0; i < n; ++i) {
+                k ^= c[i];
+                k *= 0x100000001b3ull;
+            }
+        };
+        mix(sc->nodes, sizeof(frt_node) * (size_t)sc->num_nodes);
+        mix(sc->roots, sizeof(int32_t) * (size_t)sc->num_roots);
+        mix(sc->xforms, sizeof(double) * 16 * (size_t)sc->num_xforms);
+        mix(sc->prim_data, sizeof(double) * (size_t)sc->prim_len);
+        mix(sc->materials, sizeof(frt_material) * (size_t)sc->num_materials);
+        mix(sc->patterns, sizeof(frt_pattern) * (size_t)sc->num_patterns);
+        mix(sc->textures, sizeof(frt_texture) * (size_t)sc->num_textures);
+        mix(sc->texels, sizeof(double) * (size_t)sc->texel_len);
+        mix(sc->lights, sizeof(frt_light) * (size_t)sc->num_lights);
+        mix(sc->light_points, sizeof(double) * (size_t)sc->light_point_len);
+        mix(&sc->config, sizeof(frt_config));
+        h->scene_key = k;
+    }
     phase(0);
     S.nodes = upload(h, sc->nodes, (size_t)sc->num_nodes, rc);
     S.roots = upload(h, sc->roots, (size_t)sc->num_roots, rc);
@@ -3190,9 +3224,37 @@ constexpr double kMaxGridCells = (double)(1 << 24);
 // positions | 80-byte records (binary64 position, power, pm_photon_dir of the direction bytes, heap
 // index) | cell starts | the kd-tree (binary64 position and split plane per heap index: the traversal
 // order of the estimate's selection).
-static int make_photon_map(int64_t n, const double* pos, const double* power, const uint8_t* tp,
-                           double irradiance_radius, void** out_mem, frt::PhotonMapDev& M) {
+// a photon map's device arrays, prepared on the host (make_photon_map): what every device of a process
+// uploads for the same scene and seed (shared_photon_maps)
+struct HostPhotonMap {
+    frt::PhotonMapDev M{};  // (counts, grid; the pointers are set at upload)
+    std::vector<float> pos4;
+    std::vector<double> rec, kd;
+    std::vector<int32_t> start;
+};
+
+static int upload_host_map(const HostPhotonMap& H, void** out_mem, frt::PhotonMapDev& M) {
     *out_mem = nullptr;
+    M = H.M;
+    const size_t b_pos4 = H.pos4.size() * sizeof(float), b_pw = H.rec.size() * sizeof(double);
+    const size_t b_start = H.start.size() * sizeof(int32_t), b_kd = H.kd.size() * sizeof(double);
+    const size_t o_kd = (b_pos4 + b_pw + b_start + 63) & ~(size_t)63;
+    FRT_HIP(hipMalloc(out_mem, o_kd + b_kd));
+    char* mem = (char*)*out_mem;
+    FRT_HIP(hipMemcpy(mem, H.pos4.data(), b_pos4, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4, H.rec.data(), b_pw, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + b_pos4 + b_pw, H.start.data(), b_start, hipMemcpyHostToDevice));
+    FRT_HIP(hipMemcpy(mem + o_kd, H.kd.data(), b_kd, hipMemcpyHostToDevice));
+    M.pos4 = (const float*)mem;
+    M.rec = (const double*)(mem + b_pos4);
+    M.start = (const int32_t*)(mem + b_pos4 + b_pw);
+    M.kd = (const double*)(mem + o_kd);
+    return 0;
+}
+
+static int prepare_photon_map(int64_t n, const double* pos, const double* power, const uint8_t* tp,
+                              double irradiance_radius, HostPhotonMap& H) {
+    frt::PhotonMapDev& M = H.M;
     M = frt::PhotonMapDev{};
     if (n > ((int64_t)1 << 30)) return fail("photon map too large");
     std::vector<int32_t> heap_of;
@@ -3260,8 +3322,12 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
     const size_t np = (size_t)std::max<int64_t>(nr, 1);
     const std::vector<double>& T = dir_tables();
-    std::vector<float> pos4(np * 4, 0.0f);
-    std::vector<double> rec(np * 10, 0.0), kd((size_t)(n + 1) * 4, 0.0);
+    std::vector<float>& pos4 = H.pos4;
+    std::vector<double>& rec = H.rec;
+    std::vector<double>& kd = H.kd;
+    pos4.assign(np * 4, 0.0f);
+    rec.assign(np * 10, 0.0);
+    kd.assign((size_t)(n + 1) * 4, 0.0);
     for (int64_t i = 0; i < n; ++i) {
         const int32_t hx = heap_of[(size_t)i];
         for (int k = 0; k < 3; ++k) kd[(size_t)(4 * hx + k)] = pos[3 * i + k];
@@ -3281,35 +3347,30 @@ static int make_photon_map(int64_t n, const double* pos, const double* power, co
         const int64_t hb = hx;
         std::memcpy(&rec[(size_t)(10 * j + 9)], &hb, sizeof(hb));
     }
-    const size_t b_pos4 = pos4.size() * sizeof(float), b_pw = rec.size() * sizeof(double);
-    const size_t b_start = start.size() * sizeof(int32_t), b_kd = kd.size() * sizeof(double);
-    const size_t o_kd = (b_pos4 + b_pw + b_start + 63) & ~(size_t)63;
-    FRT_HIP(hipMalloc(out_mem, o_kd + b_kd));
-    char* mem = (char*)*out_mem;
-    FRT_HIP(hipMemcpy(mem, pos4.data(), b_pos4, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4, rec.data(), b_pw, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + b_pos4 + b_pw, start.data(), b_start, hipMemcpyHostToDevice));
-    FRT_HIP(hipMemcpy(mem + o_kd, kd.data(), b_kd, hipMemcpyHostToDevice));
-    M.pos4 = (const float*)mem;
-    M.rec = (const double*)(mem + b_pos4);
-    M.start = (const int32_t*)(mem + b_pos4 + b_pw);
-    M.kd = (const double*)(mem + o_kd);
+    H.start.swap(start);
     return 0;
 }
 
-static int upload_photon_map(frt_scene_handle* h, int m, int64_t n, const double* pos, const double* power,
-                             const uint8_t* tp, double irradiance_radius) {
+static int make_photon_map(int64_t n, const double* pos, const double* power, const uint8_t* tp,
+                           double irradiance_radius, void** out_mem, frt::PhotonMapDev& M) {
+    *out_mem = nullptr;
+    HostPhotonMap H;
+    if (prepare_photon_map(n, pos, power, tp, irradiance_radius, H)) return -1;
+    return upload_host_map(H, out_mem, M);
+}
+
+static int upload_photon_map(frt_scene_handle* h, int m, const HostPhotonMap& HM) {
     auto& G = h->gi;
     hip_ignore(hipFree(G.map_mem[m]));
     G.map_mem[m] = nullptr;
     frt::PhotonMapDev M{};
-    if (make_photon_map(n, pos, power, tp, irradiance_radius, &G.map_mem[m], M)) return -1;
+    if (upload_host_map(HM, &G.map_mem[m], M)) return -1;
     h->S.pmaps[m] = M;
-    G.photons[m] = (uint64_t)n;
     return 0;
 }
 
-static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::StoredPhoton>& ph, double scale) {
+static int build_photon_map(frt_scene_handle* h, const std::vector<frt::StoredPhoton>& ph, double scale,
+                            HostPhotonMap& HM) {
     const int64_t n = (int64_t)ph.size();
     std::vector<double> pos((size_t)n * 3), power((size_t)n * 3);
     std::vector<uint8_t> tp((size_t)n * 2);
@@ -3330,30 +3391,94 @@ static int build_photon_map(frt_scene_handle* h, int m, const std::vector<frt::S
             });
         for (auto& th : pool) th.join();
     }
-    return upload_photon_map(h, m, n, pos.data(), power.data(), tp.data(), h->S.cfg.irradiance_radius);
+    return prepare_photon_map(n, pos.data(), power.data(), tp.data(), h->S.cfg.irradiance_radius, HM);
 }
+
+// The photon maps of one (scene, seed) are the same on every device (the counter RNG), so the devices of one
+// process share them: the first handle to ask traces them on its device and prepares the host arrays (the
+// balance, the grid, the records: host work on the process's CPUs), the others wait for that and upload the
+// same arrays (render_multi over N devices: one photon pass, not N on the same CPUs). Entries are keyed by
+// the scene content's hash and the seed; the last two stay (in-flight users hold their own reference), so a
+// later call with the same scene and seed (render_multi again, another handle) uploads them without a pass.
+struct SharedMaps {
+    std::mutex mu;
+    std::condition_variable cv;
+    int state = 0;  // 0 being produced, 1 ready, -1 failed
+    HostPhotonMap maps[2];
+    uint64_t photons[2] = {0, 0};
+};
+static std::mutex g_maps_mu;
+static std::vector<std::pair<std::pair<uint64_t, uint64_t>, std::shared_ptr<SharedMaps>>> g_maps;  // newest last
+
 
 // trace_photons for one render seed: caustic map 0, global map 1
 static int build_photon_maps(frt_scene_handle* h, uint64_t seed) {
     const auto& cfg = h->S.cfg;
     const int want[2] = {cfg.trace_caustic_map, cfg.trace_global_map};
     const bool timing = std::getenv("FRT_GI_TIMING") != nullptr;  // diagnostics: host-side phase times
-    for (int m = 0; m < 2; ++m) {
-        const auto t0 = std::chrono::steady_clock::now();
-        std::vector<frt::StoredPhoton> ph;
-        if (want[m])
-            for (int l = 0; l < h->S.num_lights; ++l)
-                if (trace_light_photons(h, m, l, seed, ph)) return -1;
-        // pm_store keeps at most max_photons + 1 photons (pm.c:271)
-        if ((int64_t)ph.size() > cfg.photon_count + 1) ph.resize((size_t)cfg.photon_count + 1);
-        const auto t1 = std::chrono::steady_clock::now();
-        if (build_photon_map(h, m, ph, 1.0 / (double)cfg.photon_count)) return -1;
-        if (timing) {
-            const auto t2 = std::chrono::steady_clock::now();
-            std::fprintf(stderr, "photon map %d: %zu photons, trace %.1f ms, build %.1f ms\n", m, ph.size(),
-                         std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                         std::chrono::duration<double, std::milli>(t2 - t1).count());
+    // FRT_SHARE_PHOTONS=0: every handle traces its own maps (A/B runs)
+    const bool share = !(std::getenv("FRT_SHARE_PHOTONS") && std::atoi(std::getenv("FRT_SHARE_PHOTONS")) == 0);
+    std::shared_ptr<SharedMaps> sm;
+    bool producer = true;
+    if (share) {
+        const std::pair<uint64_t, uint64_t> key(h->scene_key, seed);
+        std::lock_guard<std::mutex> lk(g_maps_mu);
+        for (auto& e : g_maps)
+            if (e.first == key) sm = e.second;
+        if (sm) {
+            producer = false;
+        } else {
+            sm = std::make_shared<SharedMaps>();
+            g_maps.emplace_back(key, sm);
+            if (g_maps.size() > 2) g_maps.erase(g_maps.begin());  // (1M-photon maps: ~130 MB of host arrays each)
         }
+    } else {
+        sm = std::make_shared<SharedMaps>();
+    }
+    if (producer) {
+        int rc = 0;
+        for (int m = 0; m < 2 && rc == 0; ++m) {
+            const auto t0 = std::chrono::steady_clock::now();
+            std::vector<frt::StoredPhoton> ph;
+            if (want[m])
+                for (int l = 0; l < h->S.num_lights && rc == 0; ++l) rc = trace_light_photons(h, m, l, seed, ph);
+            if (rc) break;
+            // pm_store keeps at most max_photons + 1 photons (pm.c:271)
+            if ((int64_t)ph.size() > cfg.photon_count + 1) ph.resize((size_t)cfg.photon_count + 1);
+            const auto t1 = std::chrono::steady_clock::now();
+            rc = build_photon_map(h, ph, 1.0 / (double)cfg.photon_count, sm->maps[m]);
+            sm->photons[m] = ph.size();
+            if (timing) {
+                const auto t2 = std::chrono::steady_clock::now();
+                std::fprintf(stderr, "photon map %d: %zu photons, trace %.1f ms, build %.1f ms\n", m, ph.size(),
+                             std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                             std::chrono::duration<double, std::milli>(t2 - t1).count());
+            }
+        }
+        g_maps_stat[0]++;
+        {
+            std::lock_guard<std::mutex> lk(sm->mu);
+            sm->state = rc ? -1 : 1;
+        }
+        sm->cv.notify_all();
+        if (rc) {  // (a later frame may try again)
+            std::lock_guard<std::mutex> lk(g_maps_mu);
+            for (size_t i = 0; i < g_maps.size(); ++i)
+                if (g_maps[i].second == sm) {
+                    g_maps.erase(g_maps.begin() + (ptrdiff_t)i);
+                    break;
+                }
+            return -1;
+        }
+    } else {
+        std::unique_lock<std::mutex> lk(sm->mu);
+        sm->cv.wait(lk, [&] { return sm->state != 0; });
+        if (sm->state < 0) return fail("photon maps: the producing device failed");
+        g_maps_stat[1]++;
+    }
+    for (int m = 0; m < 2; ++m) {
+        if (upload_photon_map(h, m, sm->maps[m])) return -1;
+        h->gi.photons[m] = sm->photons[m];
     }
     h->gi.built = true;
     h->gi.seed = seed;

@@ -231,7 +231,7 @@ __device__ __forceinline__ bool wave_scan_cells(const PhotonMapDev& M, const dou
         };
         // kScanChunks chunks per step: their position loads are all in flight before any is used
 #ifndef FRT_SCAN_CHUNKS
-#define FRT_SCAN_CHUNKS 2
+#define FRT_SCAN_CHUNKS 3  // (2: 1857 ms, 3: 1761 ms k_gather_est per cornell_gi_480x270_8x8 frame, profiles/r04_ab_gi_occupancy.txt)
 #endif
         constexpr int kScanChunks = FRT_SCAN_CHUNKS;
         for (unsigned base = 0; base < total; base += 64u * kScanChunks) {

@@ -15,7 +15,7 @@ struct frt_light;
 // (FRT_JIT_PART overrides the default, for A/B runs)
 int frt_jit_part_size();
 // the tile pair kernel (frt_jit_tile) decides runs of this many consecutive path nodes at once (a power of two
-// up to 64; 0: off; FRT_JIT_TILE overrides the default 8)
+// up to 64; 0: off; FRT_JIT_TILE overrides the default 32)
 int frt_jit_tile_size();
 // the parts (frt_jit.hip): spatially compact groups of the light's samples; returns the part count
 int frt_jit_light_parts(const frt_light& L, const double* light_points, int PS, std::vector<int32_t>& order);

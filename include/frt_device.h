@@ -284,6 +284,11 @@ int frt_jit_cache_stats(int64_t *out, int n);
  * rest (light tables, work buffers, stream), [7] total. Writes min(n, 8); returns 8. */
 int frt_upload_phases(double *out, int n);
 
+/* Counters of the photon passes since the library was loaded: out[0] photon passes traced, out[1] passes a
+ * handle took from another device's trace of the same scene and seed (render_multi over N devices traces
+ * and balances once per process). Writes min(n, 2); returns 2. */
+int frt_photon_pass_stats(int64_t *out, int n);
+
 /* Photon map entry points (parity tests; no scene needed).
  * frt_pm_balance replaces pm_balance (reference src/libs/photon_map/pm.c:329-494): the balanced
  * kd-tree of n photons given in the reference's storage order (pos: 3 doubles each); heap_of[i] = the

@@ -173,6 +173,47 @@ def test_render_multi_two_handles_on_one_device_bit_identical(built):
     assert np.array_equal(one, renderer("cornell_direct_800_4x4").render())
 
 
+def test_render_multi_shares_photon_maps_across_devices(built):
+    """render_multi over several devices of one process traces and balances the photon maps once (frt_engine.hip
+    build_photon_maps: the first handle traces, the others upload the same host arrays): the GI canvas over two
+    and three handles on device 0 equals the canvas with every handle tracing its own maps (FRT_SHARE_PHOTONS=0)
+    bit for bit, and the counters show the passes traced and shared."""
+    import ctypes
+    from fast_ray_tracer_amd.runtime import host_lib, render_multi
+    lib = host_lib()
+    lib.frt_photon_pass_stats.restype = ctypes.c_int
+
+    def passes():
+        out = (ctypes.c_int64 * 2)()
+        lib.frt_photon_pass_stats(out, 2)
+        return int(out[0]), int(out[1])
+
+    sc = load_scene("cornell_gi_24")
+    saved = {k: os.environ.get(k) for k in ("FRT_SHARE_PHOTONS", "FRT_SEED")}
+    os.environ["FRT_SEED"] = "424242"  # (a seed no other test renders this scene with: no maps kept from before)
+    try:
+        os.environ["FRT_SHARE_PHOTONS"] = "0"
+        t0, s0 = passes()
+        own = render_multi(sc, devices="0,0")  # every handle traces its own maps
+        t1, s1 = passes()
+        del os.environ["FRT_SHARE_PHOTONS"]
+        two = render_multi(sc, devices="0,0")  # one pass for both handles
+        t2, s2 = passes()
+        three = render_multi(sc, devices="0,0,0")  # the same scene and seed again: the maps are kept
+        t3, s3 = passes()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert (t1 - t0, s1 - s0) == (2, 0), (t0, s0, t1, s1)
+    assert (t2 - t1, s2 - s1) == (1, 1), (t1, s1, t2, s2)
+    assert (t3 - t2, s3 - s2) == (0, 3), (t2, s2, t3, s3)
+    assert np.isfinite(own).all() and own[:, :, :3].max() > 0
+    assert np.array_equal(own, two) and np.array_equal(own, three)
+
+
 def test_render_multi_failure_returns_zero_canvas(built):
     """The reference has no error return: a failing render_multi logs and returns a zeroed canvas
      instead of exiting the process; frt_render_multi_error names the failure (a
