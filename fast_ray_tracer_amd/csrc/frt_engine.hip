@@ -1527,6 +1527,14 @@ struct frt_scene_handle {
     void* jit_list = nullptr;          //   (frt_jit_beam_list); null: frt_jit_beam decides every pair
     int tile = 0;                      // path nodes per tile (frt_jit_tile_size), 0 without the tile kernels
     uint64_t scene_key = 0;            // hash of the flattened scene's content (shared photon maps)
+    void* jit_sub = nullptr;           // sub-part pair kernel (frt_jit_sub); null: the node pairs' rays are walked
+    int sub = 0;                       // sub-parts per part (frt_jit_sub_count) with jit_sub, else 0
+    int sub_ps = 0;                    // samples per sub-part slot (frt_jit_sub_ps)
+    const int32_t* light_psamp2 = nullptr;  // the sub-parts' samples (frt_jit_light_subparts), -1 padded
+    const float* light_sbox = nullptr;      // the sub-parts' boxes (single-row lights), binary32 outward
+    uint32_t* slist = nullptr;         // the node pairs left mixed (input of frt_jit_sub), kMixSegs segments
+    int64_t slist_cap = 0;
+    uint64_t sub_pairs = 0, sub_mixed = 0;
     float* tbox = nullptr;             // the level's tile boxes (k_prepare): 6 floats per tile
     int64_t tbox_cap = 0;
     uint32_t* tlist = nullptr;         // undecided (tile, light part) pairs, kMixSegs segments
@@ -2360,6 +2368,8 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             h->jit_tile = fns.tile;
             h->jit_list = fns.list;
             h->tile = fns.tile && fns.list ? frt_jit_tile_size() : 0;
+            h->jit_sub = fns.sub;
+            h->sub = fns.sub ? frt_jit_sub_count() : 0;
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
                 void* p = nullptr;
@@ -2409,6 +2419,45 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                 }
                 h->light_psamp = upload(h, psamp.data(), psamp.size(), rc);
                 h->light_aabb = upload(h, box.data(), box.size(), rc);
+                if (h->sub > 0) {  // the sub-parts (single-row lights): samples and boxes by (global part, sub-part)
+                    std::vector<int32_t> ps2;
+                    std::vector<float> sbox;
+                    const int Q = h->sub;
+                    size_t off = 0;
+                    for (int l = 0; l < sc->num_lights; ++l) {
+                        const frt_light& lt = sc->lights[l];
+                        const int np = std::max(1, (lt.num_samples + PS - 1) / PS);
+                        std::vector<int32_t> order(psamp.begin() + (ptrdiff_t)off, psamp.begin() + (ptrdiff_t)(off + (size_t)np * PS));
+                        off += (size_t)np * PS;
+                        std::vector<int32_t> order2;
+                        h->sub_ps = frt_jit_light_subparts(lt, sc->light_points, order, PS, Q, order2);
+                        ps2.insert(ps2.end(), order2.begin(), order2.end());
+                        for (int p = 0; p < np * Q; ++p) {
+                            double pl[3] = {INFINITY, INFINITY, INFINITY}, ph[3] = {-INFINITY, -INFINITY, -INFINITY};
+                            for (int k = 0; k < h->sub_ps; ++k) {
+                                const int q = order2[(size_t)p * h->sub_ps + k];
+                                if (q < 0) continue;
+                                const double* pt = sc->light_points + lt.points + 3 * (int64_t)q;
+                                for (int a = 0; a < 3; ++a) {
+                                    pl[a] = std::min(pl[a], pt[a]);
+                                    ph[a] = std::max(ph[a], pt[a]);
+                                }
+                            }
+                            for (int a = 0; a < 3; ++a) {
+                                float f = (float)pl[a];
+                                if ((double)f > pl[a]) f = std::nextafter(f, -INFINITY);
+                                sbox.push_back(f);
+                            }
+                            for (int a = 0; a < 3; ++a) {
+                                float f = (float)ph[a];
+                                if ((double)f < ph[a]) f = std::nextafter(f, INFINITY);
+                                sbox.push_back(f);
+                            }
+                        }
+                    }
+                    h->light_psamp2 = upload(h, ps2.data(), ps2.size(), rc);
+                    h->light_sbox = upload(h, sbox.data(), sbox.size(), rc);
+                }
                 if (rc || hipMalloc((void**)&h->mcount, frt::jit::kMixSegs * frt::jit::kMixLine * sizeof(unsigned)) != hipSuccess) {
                     frt_scene_release(h);
                     return fail("frt_scene_upload: light box / pair list allocation failed");
@@ -2528,7 +2577,7 @@ void frt_scene_release(frt_scene_handle* h) {
     if (h->jit_stats) {
         std::vector<unsigned long long> c(kJitStatWords);
         if (hipMemcpy(c.data(), h->jit_stats, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
-            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0, tpairs = 0, tmixed = 0;
+            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0, tpairs = 0, tmixed = 0, spairs = 0, smixed = 0;
             for (int j = 0; j < 64; ++j) {
                 live += c[32 * j];
                 amb += c[32 * j + 1];
@@ -2536,12 +2585,17 @@ void frt_scene_release(frt_scene_handle* h) {
                 mixed += c[32 * j + 3];
                 tpairs += c[32 * j + 4];
                 tmixed += c[32 * j + 5];
+                spairs += c[32 * j + 6];
+                smixed += c[32 * j + 7];
             }
             if (tpairs)
                 std::fprintf(stderr, "frt jit stats: tile pair kernel (%d nodes per tile): live tile pairs %llu, mixed %llu (%.2f%%)\n",
                              h->tile, tpairs, tmixed, 100.0 * (double)tmixed / (double)tpairs);
             std::fprintf(stderr, "frt jit stats: pair kernel: live pairs %llu, mixed %llu (%.2f%%)\n", pairs, mixed,
                          pairs ? 100.0 * (double)mixed / (double)pairs : 0.0);
+            if (spairs)
+                std::fprintf(stderr, "frt jit stats: sub-part pair kernel (%d sub-parts): live sub-pairs %llu, mixed %llu (%.2f%%)\n",
+                             h->sub, spairs, smixed, 100.0 * (double)smixed / (double)spairs);
             std::fprintf(stderr, "frt jit stats: live shadow lanes %llu, re-walked in binary64 %llu (%.4f%%)\n", live, amb,
                          live ? 100.0 * (double)amb / (double)live : 0.0);
             std::fprintf(stderr, "frt jit stats: (node, light) pairs: all lit %llu, all shadowed %llu, mixed %llu\n",
@@ -2595,6 +2649,7 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->shade_lcount));
     hip_ignore(hipFree(h->mixed));
     hip_ignore(hipFree(h->tlist));
+    hip_ignore(hipFree(h->slist));
     hip_ignore(hipFree(h->tbox));
     hip_ignore(hipFree(h->err));
     for (hipEvent_t e : h->ev_pool) hip_ignore(hipEventDestroy(e));
@@ -2771,7 +2826,10 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         // (FRT_JIT_MAX_PAIRS lowers the limit: the tests split small batches this way)
         const char* mp_env = std::getenv("FRT_JIT_MAX_PAIRS");
         const long long mp = mp_env ? std::atoll(mp_env) : 0;
-        const int64_t kMaxPairs = mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : (int64_t)((1ll << 31) - 1);
+        int64_t kMaxPairs = mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : (int64_t)((1ll << 31) - 1);
+        // (the sub-part pass lists (node pair) * sub + q in 32 bits)
+        const bool subbed = h->jit_beam_on && h->jit_sub && h->sub > 0 && h->light_psamp2 && h->light_sbox;
+        if (subbed) kMaxPairs = std::min<int64_t>(kMaxPairs, (int64_t)(0xFFFFFFFFull / (uint64_t)h->sub));
         if (n * NP > kMaxPairs) {
             int64_t per = std::max<int64_t>(1, kMaxPairs / NP);
             if (h->tile > 0) per = std::max<int64_t>(h->tile, per / h->tile * h->tile);
@@ -2829,11 +2887,14 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 h->tile_pairs += ntp;
                 h->tile_mixed += listed;
             }
-            // the mixed list of the node pairs: per segment, every lane of the blocks that append to it
+            // the mixed list of the node pairs: per segment, every lane of the blocks that append to it (into slist
+            // when the sub-part pass follows, else into the per-ray kernel's list)
             const int64_t pblocks = tiled ? (int64_t)list_blocks : (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
             segcap = (uint32_t)std::max<int64_t>(frt::kTraceBlock, ((pblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
+            uint32_t** nout = subbed ? &h->slist : &h->mixed;
+            int64_t& nout_cap = subbed ? h->slist_cap : h->mixed_cap;
             // pairs, then their resume values (frt_jit_rt.hpp mix_append)
-            if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
+            if (grow(nout, nout_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
                 (void)hipGetLastError();
                 h->jit_shadow = nullptr;
                 hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
@@ -2851,7 +2912,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     for (uint64_t b0 = 0; b0 < list_blocks && le == hipSuccess; b0 += max_blocks) {
                         uint32_t b0u = (uint32_t)b0;
                         void* largs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&no_box, &h->tlist, &tseg, &b0u,
-                                         &tsegcap, &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap, &h->err,
+                                         &tsegcap, &h->light_aabb, &counts, nout, &h->mcount, &segcap, &h->err,
                                          &h->jit_stats};
                         le = hipModuleLaunchKernel((hipFunction_t)h->jit_list, (unsigned)std::min(max_blocks, list_blocks - b0), 1, 1,
                                                    frt::kTraceBlock, 1, 1, 0, h->stream, largs, nullptr);
@@ -2864,7 +2925,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     frt::jit::SegTable no_seg{};
                     uint32_t zero = 0;
                     void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &nn, (void*)&no_box, (void*)&no_list, &no_seg, &zero, &zero,
-                                     &h->light_aabb, &counts, &h->mixed, &h->mcount, &segcap, &h->err, &h->jit_stats};
+                                     &h->light_aabb, &counts, nout, &h->mcount, &segcap, &h->err, &h->jit_stats};
                     le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1, 1,
                                                frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
                     h->node_pairs += (uint64_t)npairs;
@@ -2885,6 +2946,59 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 return;
             for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
             h->node_mixed += total_mixed;
+            if (subbed && total_mixed > 0) {
+                // the sub-part pass: sub lanes per node pair left mixed, the sub-parts' beams resumed from its point
+                frt::jit::SegTable sseg{};
+                uint64_t listed_n = 0;
+                const uint64_t sblocks = seg_table(h->host_mcount, segcap, (uint64_t)h->sub, sseg, listed_n);
+                uint32_t nsegcap = segcap;  // (the node list's capacity: its layout)
+                uint32_t ssegcap = (uint32_t)std::max<uint64_t>(frt::kTraceBlock,
+                                                                ((sblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
+                if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)ssegcap * kMixSegs)) {  // (out of memory): the generic walk
+                    (void)hipGetLastError();
+                    h->jit_shadow = nullptr;
+                    hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                    launch_shadow(h, B, rec, n, counts, node0);
+                    return;
+                }
+                hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
+                hipError_t se = hipSuccess;
+                {
+                    KTimer ts(h, h->cur_st, 13);
+                    const uint64_t max_blocks = ((1ull << 31) - 1) / frt::kTraceBlock;
+                    uint32_t zero = 0;
+                    for (uint64_t b0 = 0; b0 < sblocks && se == hipSuccess; b0 += max_blocks) {
+                        uint32_t b0u = (uint32_t)b0;
+                        void* sargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&h->light_sbox, &h->slist, &sseg, &b0u,
+                                         &nsegcap, &h->light_aabb, &counts, &h->mixed, &h->mcount, &ssegcap, &h->err,
+                                         &h->jit_stats};
+                        se = hipModuleLaunchKernel((hipFunction_t)h->jit_sub, (unsigned)std::min(max_blocks, sblocks - b0), 1, 1,
+                                                   frt::kTraceBlock, 1, 1, 0, h->stream, sargs, nullptr);
+                    }
+                }
+                if (se != hipSuccess) {
+                    std::fprintf(stderr, "frt: scene-specialised sub-part kernel launch failed (%s); pairs per ray\n",
+                                 hipGetErrorString(se));
+                    (void)hipGetLastError();
+                    h->jit_sub = nullptr;
+                    h->sub = 0;
+                    hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                    launch_shadow(h, B, rec, n, counts, node0);
+                    return;
+                }
+                if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                                   hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                    hipStreamSynchronize(h->stream) != hipSuccess)
+                    return;
+                h->sub_pairs += listed_n * (uint64_t)h->sub;
+                segcap = ssegcap;
+                total_mixed = 0;
+                for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
+                h->sub_mixed += total_mixed;
+            } else if (subbed) {
+                // (nothing left mixed: the per-ray kernel's list is empty)
+                std::fill(h->host_mcount.begin(), h->host_mcount.end(), 0u);
+            }
         } else {
             segcap = (uint32_t)std::max<int64_t>(1, npairs);
             if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
@@ -2896,8 +3010,10 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
             total_mixed = (uint64_t)npairs;  // every pair, in order (frt_jit_shadow's all_pairs)
         }
         uint32_t all_pairs = h->jit_beam_on ? 0u : 1u;
-        // lanes per pair (a part of frt_jit_part_size() samples); tid / lpp by multiply-shift
-        uint32_t lpp = (uint32_t)frt_jit_part_size();
+        // lanes per pair (a part of frt_jit_part_size() samples, or a sub-part's slot after frt_jit_sub);
+        // tid / lpp by multiply-shift
+        uint32_t subq = subbed ? 1u : 0u;
+        uint32_t lpp = subbed ? (uint32_t)h->sub_ps : (uint32_t)frt_jit_part_size();
         uint32_t shift = 32;
         while ((1u << (shift - 32)) < lpp) ++shift;  // 32 + ceil(log2 lpp)
         const uint64_t magic = (uint64_t)((((unsigned __int128)1 << shift) + lpp - 1) / lpp);
@@ -2932,7 +3048,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 grid = std::min<uint64_t>(max_blocks, nblk - b0);
             }
             void* args[] = {&h->S, (void*)&B, (void*)&rec, &total, &m0, &h->mixed, &seg, &b0, &segcap, &all_pairs,
-                            &h->light_psamp, &lpp, (void*)&magic,
+                            &h->light_psamp, &subq, &h->light_psamp2, &lpp, (void*)&magic,
                             &shift, &spn, &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
             const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, (unsigned)grid,
                                                         1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
@@ -3597,7 +3713,7 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
     h->cur_st = st;
     h->rays_walked = 0;
     h->pairs_walked = 0;
-    h->tile_pairs = h->tile_mixed = h->node_pairs = h->node_mixed = 0;
+    h->tile_pairs = h->tile_mixed = h->node_pairs = h->node_mixed = h->sub_pairs = h->sub_mixed = 0;
     const int rc = render_frame(h, P, dev_out, st);
     if (rc) h->gi.built = false;
     return rc;
@@ -3846,6 +3962,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->shadow_tile_mixed = h->tile_mixed;
         st->shadow_pairs = h->node_pairs;
         st->shadow_pairs_mixed = h->node_mixed;
+        st->shadow_sub_pairs = h->sub_pairs;
+        st->shadow_sub_mixed = h->sub_mixed;
         collect_timings(h, st);
     }
 #if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)

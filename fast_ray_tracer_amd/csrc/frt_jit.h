@@ -17,6 +17,13 @@ int frt_jit_part_size();
 // the tile pair kernel (frt_jit_tile) decides runs of this many consecutive path nodes at once (a power of two
 // up to 64; 0: off; FRT_JIT_TILE overrides the default 32)
 int frt_jit_tile_size();
+// the sub-part pass (frt_jit_sub) splits the parts of the node pairs left mixed into this many sub-parts (2, 4 or
+// 8; 0: off, the default; FRT_JIT_SUB=n turns it on); their sizes, the largest (PS2), and the sub-parts' samples
+int frt_jit_sub_count();
+std::vector<int> frt_jit_sub_sizes(int c, int Q);
+int frt_jit_sub_ps(int PS, int Q);
+int frt_jit_light_subparts(const frt_light& L, const double* light_points, const std::vector<int32_t>& order, int PS,
+                           int Q, std::vector<int32_t>& order2);
 // the parts (frt_jit.hip): spatially compact groups of the light's samples; returns the part count
 int frt_jit_light_parts(const frt_light& L, const double* light_points, int PS, std::vector<int32_t>& order);
 
@@ -31,6 +38,7 @@ struct FrtJitFns {
     void* beam = nullptr;    // frt_jit_beam: every (node, part) pair
     void* tile = nullptr;    // frt_jit_tile: every (tile, part) pair
     void* list = nullptr;    // frt_jit_beam_list: the nodes of the listed tile pairs
+    void* sub = nullptr;     // frt_jit_sub: the sub-parts of the node pairs left mixed
 };
 // compile with hiprtc for `device` (cached per device and source); 0 on success
 int frt_jit_compile(const std::string& src, int device, FrtJitFns& fns, std::string& log);

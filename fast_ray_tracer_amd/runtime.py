@@ -39,11 +39,12 @@ class FrameStats(ctypes.Structure):
                 ("sub_ms", ctypes.c_double * 8), ("sub_launches", ctypes.c_uint64 * 8),
                 ("shadow_rays_walked", ctypes.c_uint64), ("shadow_tile_pairs", ctypes.c_uint64),
                 ("shadow_tile_mixed", ctypes.c_uint64), ("shadow_pairs", ctypes.c_uint64),
-                ("shadow_pairs_mixed", ctypes.c_uint64)]
+                ("shadow_pairs_mixed", ctypes.c_uint64), ("shadow_sub_pairs", ctypes.c_uint64),
+                ("shadow_sub_mixed", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
-        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile"]
+        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile", "frt_jit_sub"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
@@ -59,6 +60,7 @@ class FrameStats(ctypes.Structure):
             "shadow_rays_walked": int(self.shadow_rays_walked),
             "shadow_tile_pairs": int(self.shadow_tile_pairs), "shadow_tile_mixed": int(self.shadow_tile_mixed),
             "shadow_pairs": int(self.shadow_pairs), "shadow_pairs_mixed": int(self.shadow_pairs_mixed),
+            "shadow_sub_pairs": int(self.shadow_sub_pairs), "shadow_sub_mixed": int(self.shadow_sub_mixed),
         }
 
 

@@ -111,3 +111,46 @@ def test_pair_kernel_batches_split_by_node_range(built, name):
         del os.environ["FRT_JIT_MAX_PAIRS"]
     assert st_a.shadow_jit == 1 and st_b.shadow_jit == 1
     assert np.array_equal(img_a, img_b)
+
+
+_ENV_RENDER = r"""
+import sys, numpy as np
+sys.path.insert(0, {tests!r})
+from conftest import load_scene
+from fast_ray_tracer_amd.runtime import GpuRenderer
+r = GpuRenderer(load_scene({name!r}))
+img, st = r.render(stats=True)
+d = st.as_dict()
+np.save({out!r}, img)
+print("STATS", d["shadow_jit"], d["shadow_tile_pairs"], d["shadow_sub_pairs"])
+"""
+
+
+def _render_env_process(name, env, out):
+    """Render in a fresh process (the tile size and sub-part count are read once per process)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = subprocess.run([sys.executable, "-c", _ENV_RENDER.format(tests=here, name=name, out=str(out))],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    stats = [ln.split()[1:] for ln in p.stdout.splitlines() if ln.startswith("STATS")][-1]
+    return np.load(str(out)), [int(x) for x in stats]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "reflect_refract_test_150", "test_scene_120"])
+def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
+    """The tile pair kernel (frt_jit_tile: runs of consecutive path nodes from their origin box, then
+    frt_jit_beam_list for the nodes of the tiles left) at several tile sizes, the sub-part pass (frt_jit_sub,
+    off by default) and the tile path split into node ranges (FRT_JIT_MAX_PAIRS: ranges start at tile
+    boundaries): each canvas equals the generic walk's bit for bit, and the kernels in question ran."""
+    ref, st = _render_env_process(name, {"FRT_JIT": "0"}, tmp_path / "g.npy")
+    assert st[0] == 0
+    for i, env in enumerate(({"FRT_JIT_TILE": "2"}, {"FRT_JIT_TILE": "32"}, {"FRT_JIT_TILE": "64", "FRT_JIT_SUB": "4"},
+                             {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"})):
+        img, st = _render_env_process(name, env, tmp_path / ("j%d.npy" % i))
+        assert st[0] == 1 and st[1] > 0, (env, st)
+        if "FRT_JIT_SUB" in env:
+            assert st[2] > 0, (env, st)
+        assert np.array_equal(img, ref), env
