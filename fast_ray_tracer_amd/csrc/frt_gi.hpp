@@ -407,6 +407,12 @@ __device__ __forceinline__ void radix_pick(const unsigned* c4, unsigned need, un
     below = (unsigned)__builtin_amdgcn_readlane((int)b, owner);
 }
 
+// the sum passes' record chunks in flight per round trip (80 bytes per lane each)
+#ifndef FRT_SUM_CHUNKS
+#define FRT_SUM_CHUNKS 2
+#endif
+constexpr int kSumChunks = FRT_SUM_CHUNKS;
+
 // all 64 lanes call with the same x / normal; returns the photons used (the reference's `found`) and
 // the irradiance, in every lane
 __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& M, const double* x, const double* normal,
@@ -606,18 +612,22 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
         irrad[2] *= tmp;
     };
     if (total <= (unsigned)k) {  // every photon in range: no heap, dist2[0] = max_dist^2
-        if (listed) {  // two chunks of the list per round trip
-            for (unsigned base = 0; base < count; base += 128) {
-                const unsigned i0 = base + (unsigned)lane, i1 = i0 + 64u;
-                const bool a = i0 < count, b = i1 < count;
-                const int32_t pa = a ? (int32_t)L.ent[i0].y : 0, pb = b ? (int32_t)L.ent[i1].y : 0;
-                EST_LANES(15, a);
-                EST_LANES(15, b);
-                PhotonRec ra, rb;
-                if (a) ra = photon_rec(M, pa);
-                if (b) rb = photon_rec(M, pb);
-                if (a) accumulate(ra, pa, sqrt_w(ra.d2(x)));
-                if (b) accumulate(rb, pb, sqrt_w(rb.d2(x)));
+        if (listed) {  // kSumChunks chunks of the list per round trip
+            for (unsigned base = 0; base < count; base += 64u * kSumChunks) {
+                PhotonRec rc[kSumChunks];
+                bool ok[kSumChunks];
+                int32_t pc[kSumChunks];
+#pragma unroll
+                for (int c = 0; c < kSumChunks; ++c) {
+                    const unsigned i = base + 64u * c + (unsigned)lane;
+                    ok[c] = i < count;
+                    pc[c] = ok[c] ? (int32_t)L.ent[i].y : 0;
+                    EST_LANES(15, ok[c]);
+                    if (ok[c]) rc[c] = photon_rec(M, pc[c]);
+                }
+#pragma unroll
+                for (int c = 0; c < kSumChunks; ++c)
+                    if (ok[c]) accumulate(rc[c], pc[c], sqrt_w(rc[c].d2(x)));
             }
         } else {
             visit([&](int32_t p, bool in, unsigned) {
@@ -762,23 +772,24 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     // loads issue with near_mask's
     const unsigned qmask = near_mask(M.kd, R, x);
     if (compact) {
-        for (unsigned base = 0; base < c_in; base += 128) {
-            const unsigned i0 = base + (unsigned)lane, i1 = i0 + 64u;
-            const bool a = i0 < c_in, b = i1 < c_in;
-            PhotonRec ra, rb;
-            const int32_t pa = a ? (int32_t)L.sel[i0] : 0, pb = b ? (int32_t)L.sel[i1] : 0;
-            EST_LANES(15, a);
-            EST_LANES(15, b);
-            if (a) ra = photon_rec(M, pa);
-            if (b) rb = photon_rec(M, pb);
-            if (a) {
-                accumulate(ra, pa, sqrt_w(ra.d2(x)));
-                before_all = before_all && found_before(ra.heap(), R, qmask);
+        for (unsigned base = 0; base < c_in; base += 64u * kSumChunks) {
+            PhotonRec rc[kSumChunks];
+            bool ok[kSumChunks];
+            int32_t pc[kSumChunks];
+#pragma unroll
+            for (int c = 0; c < kSumChunks; ++c) {
+                const unsigned i = base + 64u * c + (unsigned)lane;
+                ok[c] = i < c_in;
+                pc[c] = ok[c] ? (int32_t)L.sel[i] : 0;
+                EST_LANES(15, ok[c]);
+                if (ok[c]) rc[c] = photon_rec(M, pc[c]);
             }
-            if (b) {
-                accumulate(rb, pb, sqrt_w(rb.d2(x)));
-                before_all = before_all && found_before(rb.heap(), R, qmask);
-            }
+#pragma unroll
+            for (int c = 0; c < kSumChunks; ++c)
+                if (ok[c]) {
+                    accumulate(rc[c], pc[c], sqrt_w(rc[c].d2(x)));
+                    before_all = before_all && found_before(rc[c].heap(), R, qmask);
+                }
         }
     }
     if (!compact || !fast) visit([&](int32_t p, bool in, unsigned key) {

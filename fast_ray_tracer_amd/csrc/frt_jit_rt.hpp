@@ -628,7 +628,8 @@ __device__ __forceinline__ bool beam_axis(float thr, float bmax, float sig, cons
 // misses); thr: the EPSILON thresholds, bmax >= |B|, sig: the permutation remnants (kSig)
 template <bool kSig, typename BW>
 __device__ __forceinline__ bool beam_slabs(const float* thr, float bmax, float sig, const BW& w, const float* B0,
-                                           const float* B1, Iv& tmin, Iv& tmax) {
+                                           const float* B1, Iv& tmin, Iv& tmax, Iv* amn = nullptr, Iv* amx = nullptr,
+                                           bool* aok = nullptr) {
     bool ok = true, split_ok = true, any_ok = false;
     float snear = 0.0f;  // max over the split axes
     Iv smin{-__builtin_huge_valf(), -__builtin_huge_valf()}, smax{__builtin_huge_valf(), __builtin_huge_valf()};
@@ -636,6 +637,11 @@ __device__ __forceinline__ bool beam_slabs(const float* thr, float bmax, float s
     for (int a = 0; a < 3; ++a) {
         Iv mn, mx;
         const bool oka = beam_axis<kSig>(thr[a], bmax, sig, w, a, B0[a], B1[a], mn, mx);
+        if (amn != nullptr) {  // (the axes' own intervals: cube_iv_meta)
+            amn[a] = mn;
+            amx[a] = mx;
+            aok[a] = oka;
+        }
         ok = oka && ok;
         if (oka) {  // the decided axes alone
             smin = Iv{fmaxf(smin.lo, mn.lo), fmaxf(smin.hi, mn.hi)};
@@ -893,6 +899,69 @@ template <int kAa, typename W>
 __device__ __forceinline__ int cube_iv(const Node32& nd, const W& w, Iv& t0, Iv& t1) {
     if (!cube_slab<kAa>(nd, w, t0, t1)) return -1;
     return iv_le(t0, t1);
+}
+
+// ---- the order of two slab values on one axis (beams) ----
+// Two cubes' entries (or exits) that come, for every ray of a beam, from slab planes on the same axis a are
+// (B_i - o_a) / d_a and (B_j - o_a) / d_a for the same ray (axis-aligned frames: the local slab value is
+// exactly that in real arithmetic, the reference's binary64 roundings ~2^-50 relative): their order is the
+// sign of (B_j - B_i) d_a for every ray at once, however widely the beam spreads each value. The interval
+// walk alone loses that correlation: on the headline frame the window wall's two slabs and its hole order
+// their x-faces 0.001-0.0025 apart, less than the spread of one part's beam.
+struct SlabMeta {
+    int ax;    // the axis giving this entry / exit for every ray of the beam, -1 none known
+    float B;   // its plane (world, binary32)
+    bool pos;  // the beam's direction along it (sign-definite: a binding axis is)
+};
+
+// cube_iv on a beam, with the binding axes of the entry (m0) and the exit (m1): axis a binds the entry when
+// its interval lies above every other axis's (the reference's max over axes is then a's value, or an equal
+// one), the exit when below every other's
+template <int kAa, typename BW>
+__device__ __forceinline__ int cube_iv_meta(const Node32& nd, const BW& w, Iv& t0, Iv& t1, SlabMeta& m0, SlabMeta& m1) {
+    m0.ax = m1.ax = -1;
+    m0.B = m1.B = 0.0f;
+    m0.pos = m1.pos = false;
+    if (kAa == 0) {  // (own frames take no beam decision)
+        t0 = t1 = Iv{0.0f, 0.0f};
+        return -1;
+    }
+    Iv mn[3], mx[3];
+    bool ok[3];
+    // (the decision itself: beam_slabs, as aa_slab / cube_iv)
+    if (!beam_slabs<kAa == 2>(nd.aathr, nd.aabmax, nd.aasig, w, nd.aab, nd.aab + 3, t0, t1, mn, mx, ok)) return -1;
+    const int x = iv_le(t0, t1);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
+        const bool pos = w.Dlo[a] > 0.0f;
+        const float Bl = fminf(nd.aab[a], nd.aab[a + 3]), Bh = fmaxf(nd.aab[a], nd.aab[a + 3]);
+        if (ok[a] && mn[a].lo >= mn[b].hi && mn[a].lo >= mn[c].hi) {
+            m0.ax = a;
+            m0.B = pos ? Bl : Bh;
+            m0.pos = pos;
+        }
+        if (ok[a] && mx[a].hi <= mx[b].lo && mx[a].hi <= mx[c].lo) {
+            m1.ax = a;
+            m1.B = pos ? Bh : Bl;
+            m1.pos = pos;
+        }
+    }
+    return x;
+}
+
+// the order of slab values a, b known by their planes: 1 certainly t_a <= t_b, 0 certainly t_a > t_b, -1
+// unknown. The planes are binary32 roundings (u |B| each) of the reference's; the reference's own values err by
+// ~2^-50 relative (slack: 2^-30 (|B| + max|o|)); a permutation's remnants move a slab value by up to
+// 1.0001 sigma (|o| + |t|) / |d_a| (sigma = nd.aasig of either cube: both are passed as sig, the larger)
+template <typename BW>
+__device__ __forceinline__ int slab_order(const SlabMeta& a, const SlabMeta& b, float sig, float tmax, const BW& w) {
+    if (a.ax < 0 || a.ax != b.ax) return -1;
+    const float d = b.B - a.B;
+    const float m = 1.02f * kU * (fabsf(a.B) + fabsf(b.B) + fabsf(d)) + 0x1p-30f * (fabsf(a.B) + fabsf(b.B) + w.omax) +
+                    2.02f * sig * (w.omax + tmax * w.Dn);
+    if (!(fabsf(d) > m)) return -1;
+    return (d > 0.0f) == a.pos ? 1 : 0;  // (a.pos: no indexing of the beam by a lane value, which would spill it)
 }
 
 // a cube outside CSG units: leaf_top's decisions on intervals, as lane masks; undecided -> amb.

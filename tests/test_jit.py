@@ -143,11 +143,13 @@ def _render_env_process(name, env, out):
 def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
     """The tile pair kernel (frt_jit_tile: runs of consecutive path nodes from their origin box, then
     frt_jit_beam_list for the nodes of the tiles left) at several tile sizes, the sub-part pass (frt_jit_sub,
-    off by default) and the tile path split into node ranges (FRT_JIT_MAX_PAIRS: ranges start at tile
+    off by default), the same-axis slab order (jit::slab_order: tile kernel by default, FRT_JIT_ORDER 0 none, 2 every
+    pair kernel) and the tile path split into node ranges (FRT_JIT_MAX_PAIRS: ranges start at tile
     boundaries): each canvas equals the generic walk's bit for bit, and the kernels in question ran."""
     ref, st = _render_env_process(name, {"FRT_JIT": "0"}, tmp_path / "g.npy")
     assert st[0] == 0
-    for i, env in enumerate(({"FRT_JIT_TILE": "2"}, {"FRT_JIT_TILE": "32"}, {"FRT_JIT_TILE": "64", "FRT_JIT_SUB": "4"},
+    for i, env in enumerate(({"FRT_JIT_TILE": "2"}, {"FRT_JIT_TILE": "32"}, {"FRT_JIT_TILE": "32", "FRT_JIT_ORDER": "0"},
+                             {"FRT_JIT_TILE": "64", "FRT_JIT_SUB": "4", "FRT_JIT_ORDER": "2"},
                              {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"})):
         img, st = _render_env_process(name, env, tmp_path / ("j%d.npy" % i))
         assert st[0] == 1 and st[1] > 0, (env, st)
