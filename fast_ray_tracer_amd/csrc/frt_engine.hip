@@ -2827,8 +2827,9 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         const char* mp_env = std::getenv("FRT_JIT_MAX_PAIRS");
         const long long mp = mp_env ? std::atoll(mp_env) : 0;
         int64_t kMaxPairs = mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : (int64_t)((1ll << 31) - 1);
-        // (the sub-part pass lists (node pair) * sub + q in 32 bits)
-        const bool subbed = h->jit_beam_on && h->jit_sub && h->sub > 0 && h->light_psamp2 && h->light_sbox;
+        // (the sub-part pass after the tile kernel: the per-ray kernel's list holds (node pair) * sub + q in 32 bits)
+        const bool tiled = h->jit_beam_on && h->tile > 0 && h->jit_tile && h->jit_list && h->tbox;
+        const bool subbed = tiled && h->jit_sub && h->sub > 0 && h->light_psamp2 && h->light_sbox;
         if (subbed) kMaxPairs = std::min<int64_t>(kMaxPairs, (int64_t)(0xFFFFFFFFull / (uint64_t)h->sub));
         if (n * NP > kMaxPairs) {
             int64_t per = std::max<int64_t>(1, kMaxPairs / NP);
@@ -2838,7 +2839,6 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
             return;
         }
         const int64_t npairs = n * NP;
-        const bool tiled = h->jit_beam_on && h->tile > 0 && h->jit_tile && h->jit_list && h->tbox;
         uint32_t nn = (uint32_t)n;
         uint32_t segcap = 0;
         uint64_t total_mixed = 0;
@@ -2846,6 +2846,10 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
             frt::jit::SegTable tseg{};
             uint32_t tsegcap = 0;
             uint64_t list_blocks = 0, listed = 0;
+            // the node pair kernel's input (tiled): the tile pairs left mixed, or the tile sub-pairs left mixed
+            const uint32_t* list_in = h->tlist;
+            uint32_t list_segcap = 0;
+            const float* list_boxes = h->light_aabb;
             int tl = 0;
             while ((1 << tl) < h->tile) ++tl;
             if (tiled) {
@@ -2883,16 +2887,73 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                                    hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                     hipStreamSynchronize(h->stream) != hipSuccess)
                     return;
-                list_blocks = seg_table(h->host_mcount, tsegcap, (uint64_t)h->tile, tseg, listed);
+                list_blocks = seg_table(h->host_mcount, tsegcap, subbed ? (uint64_t)h->sub : (uint64_t)h->tile, tseg, listed);
                 h->tile_pairs += ntp;
                 h->tile_mixed += listed;
+                list_in = h->tlist;
+                list_segcap = tsegcap;
+                if (subbed && listed > 0) {
+                    // the sub-part pass: sub lanes per tile pair left mixed, the tile's beam to each sub-part's box
+                    // resumed from the tile pair's point; the sub-pairs it leaves go to the node pair kernel
+                    const uint64_t sblocks = list_blocks;
+                    const frt::jit::SegTable sseg = tseg;
+                    const uint32_t ssegcap = (uint32_t)std::max<uint64_t>(frt::kTraceBlock,
+                                                                          ((sblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
+                    if (grow(&h->slist, h->slist_cap, 2 * (int64_t)ssegcap * kMixSegs)) {  // (out of memory): the generic walk
+                        (void)hipGetLastError();
+                        h->jit_shadow = nullptr;
+                        hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                        launch_shadow(h, B, rec, n, counts, node0);
+                        return;
+                    }
+                    hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
+                    hipError_t se = hipSuccess;
+                    {
+                        KTimer ts(h, h->cur_st, 13);
+                        const uint64_t max_blocks = ((1ull << 31) - 1) / frt::kTraceBlock;
+                        uint32_t zero = 0;
+                        for (uint64_t b0 = 0; b0 < sblocks && se == hipSuccess; b0 += max_blocks) {
+                            uint32_t b0u = (uint32_t)b0;
+                            void* sargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&tb, &h->tlist, (void*)&sseg, &b0u,
+                                             &tsegcap, &h->light_sbox, &counts, &h->slist, &h->mcount, (void*)&ssegcap, &h->err,
+                                             &h->jit_stats};
+                            se = hipModuleLaunchKernel((hipFunction_t)h->jit_sub, (unsigned)std::min(max_blocks, sblocks - b0), 1, 1,
+                                                       frt::kTraceBlock, 1, 1, 0, h->stream, sargs, nullptr);
+                        }
+                    }
+                    if (se != hipSuccess) {
+                        std::fprintf(stderr, "frt: scene-specialised sub-part kernel launch failed (%s); no sub-parts\n",
+                                     hipGetErrorString(se));
+                        (void)hipGetLastError();
+                        h->jit_sub = nullptr;
+                        h->sub = 0;
+                        hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                        launch_shadow(h, B, rec, n, counts, node0);
+                        return;
+                    }
+                    if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                                       hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                        hipStreamSynchronize(h->stream) != hipSuccess)
+                        return;
+                    uint64_t listed_s = 0;
+                    list_blocks = seg_table(h->host_mcount, ssegcap, (uint64_t)h->tile, tseg, listed_s);
+                    h->sub_pairs += listed * (uint64_t)h->sub;
+                    h->sub_mixed += listed_s;
+                    listed = listed_s;
+                    list_in = h->slist;
+                    list_segcap = ssegcap;
+                    list_boxes = h->light_sbox;
+                } else if (subbed) {
+                    list_blocks = 0;  // (no tile pair left)
+                    listed = 0;
+                }
             }
-            // the mixed list of the node pairs: per segment, every lane of the blocks that append to it (into slist
-            // when the sub-part pass follows, else into the per-ray kernel's list)
+            // the mixed list of the node pairs (the per-ray kernel's): per segment, every lane of the blocks that
+            // append to it
             const int64_t pblocks = tiled ? (int64_t)list_blocks : (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
             segcap = (uint32_t)std::max<int64_t>(frt::kTraceBlock, ((pblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
-            uint32_t** nout = subbed ? &h->slist : &h->mixed;
-            int64_t& nout_cap = subbed ? h->slist_cap : h->mixed_cap;
+            uint32_t** nout = &h->mixed;
+            int64_t& nout_cap = h->mixed_cap;
             // pairs, then their resume values (frt_jit_rt.hpp mix_append)
             if (grow(nout, nout_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
                 (void)hipGetLastError();
@@ -2911,8 +2972,8 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     uint32_t zero = 0;
                     for (uint64_t b0 = 0; b0 < list_blocks && le == hipSuccess; b0 += max_blocks) {
                         uint32_t b0u = (uint32_t)b0;
-                        void* largs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&no_box, &h->tlist, &tseg, &b0u,
-                                         &tsegcap, &h->light_aabb, &counts, nout, &h->mcount, &segcap, &h->err,
+                        void* largs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&no_box, (void*)&list_in, &tseg, &b0u,
+                                         &list_segcap, (void*)&list_boxes, &counts, nout, &h->mcount, &segcap, &h->err,
                                          &h->jit_stats};
                         le = hipModuleLaunchKernel((hipFunction_t)h->jit_list, (unsigned)std::min(max_blocks, list_blocks - b0), 1, 1,
                                                    frt::kTraceBlock, 1, 1, 0, h->stream, largs, nullptr);
@@ -2946,59 +3007,6 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 return;
             for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
             h->node_mixed += total_mixed;
-            if (subbed && total_mixed > 0) {
-                // the sub-part pass: sub lanes per node pair left mixed, the sub-parts' beams resumed from its point
-                frt::jit::SegTable sseg{};
-                uint64_t listed_n = 0;
-                const uint64_t sblocks = seg_table(h->host_mcount, segcap, (uint64_t)h->sub, sseg, listed_n);
-                uint32_t nsegcap = segcap;  // (the node list's capacity: its layout)
-                uint32_t ssegcap = (uint32_t)std::max<uint64_t>(frt::kTraceBlock,
-                                                                ((sblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
-                if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)ssegcap * kMixSegs)) {  // (out of memory): the generic walk
-                    (void)hipGetLastError();
-                    h->jit_shadow = nullptr;
-                    hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
-                    launch_shadow(h, B, rec, n, counts, node0);
-                    return;
-                }
-                hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
-                hipError_t se = hipSuccess;
-                {
-                    KTimer ts(h, h->cur_st, 13);
-                    const uint64_t max_blocks = ((1ull << 31) - 1) / frt::kTraceBlock;
-                    uint32_t zero = 0;
-                    for (uint64_t b0 = 0; b0 < sblocks && se == hipSuccess; b0 += max_blocks) {
-                        uint32_t b0u = (uint32_t)b0;
-                        void* sargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&h->light_sbox, &h->slist, &sseg, &b0u,
-                                         &nsegcap, &h->light_aabb, &counts, &h->mixed, &h->mcount, &ssegcap, &h->err,
-                                         &h->jit_stats};
-                        se = hipModuleLaunchKernel((hipFunction_t)h->jit_sub, (unsigned)std::min(max_blocks, sblocks - b0), 1, 1,
-                                                   frt::kTraceBlock, 1, 1, 0, h->stream, sargs, nullptr);
-                    }
-                }
-                if (se != hipSuccess) {
-                    std::fprintf(stderr, "frt: scene-specialised sub-part kernel launch failed (%s); pairs per ray\n",
-                                 hipGetErrorString(se));
-                    (void)hipGetLastError();
-                    h->jit_sub = nullptr;
-                    h->sub = 0;
-                    hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
-                    launch_shadow(h, B, rec, n, counts, node0);
-                    return;
-                }
-                if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
-                                   hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-                    hipStreamSynchronize(h->stream) != hipSuccess)
-                    return;
-                h->sub_pairs += listed_n * (uint64_t)h->sub;
-                segcap = ssegcap;
-                total_mixed = 0;
-                for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
-                h->sub_mixed += total_mixed;
-            } else if (subbed) {
-                // (nothing left mixed: the per-ray kernel's list is empty)
-                std::fill(h->host_mcount.begin(), h->host_mcount.end(), 0u);
-            }
         } else {
             segcap = (uint32_t)std::max<int64_t>(1, npairs);
             if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk

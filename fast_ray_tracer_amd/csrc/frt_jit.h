@@ -15,10 +15,11 @@ struct frt_light;
 // (FRT_JIT_PART overrides the default, for A/B runs)
 int frt_jit_part_size();
 // the tile pair kernel (frt_jit_tile) decides runs of this many consecutive path nodes at once (a power of two
-// up to 64; 0: off; FRT_JIT_TILE overrides the default 32)
+// up to 64; 0: off; FRT_JIT_TILE overrides the default 64)
 int frt_jit_tile_size();
-// the sub-part pass (frt_jit_sub) splits the parts of the node pairs left mixed into this many sub-parts (2, 4 or
-// 8; 0: off, the default; FRT_JIT_SUB=n turns it on); their sizes, the largest (PS2), and the sub-parts' samples
+// the sub-part pass (frt_jit_sub, after the tile kernel) splits the parts of the tile pairs left mixed into this many
+// sub-parts (2 ... 32; 0: off; FRT_JIT_SUB overrides the default 16); their sizes, the largest (PS2), and the
+// sub-parts' samples
 int frt_jit_sub_count();
 std::vector<int> frt_jit_sub_sizes(int c, int Q);
 int frt_jit_sub_ps(int PS, int Q);

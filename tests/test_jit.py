@@ -141,18 +141,20 @@ def _render_env_process(name, env, out):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "reflect_refract_test_150", "test_scene_120"])
 def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
-    """The tile pair kernel (frt_jit_tile: runs of consecutive path nodes from their origin box, then
-    frt_jit_beam_list for the nodes of the tiles left) at several tile sizes, the sub-part pass (frt_jit_sub,
-    off by default), the same-axis slab order (jit::slab_order: tile kernel by default, FRT_JIT_ORDER 0 none, 2 every
-    pair kernel) and the tile path split into node ranges (FRT_JIT_MAX_PAIRS: ranges start at tile
-    boundaries): each canvas equals the generic walk's bit for bit, and the kernels in question ran."""
+    """The tile pair kernel (frt_jit_tile: runs of consecutive path nodes from their origin box), the sub-part pass
+    after it (frt_jit_sub: the tile pairs left mixed, their parts split into sub-parts; 16 single samples of the
+    16-sample parts by default, FRT_JIT_SUB=0 off) and frt_jit_beam_list for the nodes of the tile (sub-)pairs left,
+    at several tile, part and sub-part sizes, the same-axis slab order (jit::slab_order: tile kernels by default,
+    FRT_JIT_ORDER 0 none, 2 every pair kernel) and the tile path split into node ranges (FRT_JIT_MAX_PAIRS: ranges
+    start at tile boundaries): each canvas equals the generic walk's bit for bit, and the kernels in question ran."""
     ref, st = _render_env_process(name, {"FRT_JIT": "0"}, tmp_path / "g.npy")
     assert st[0] == 0
-    for i, env in enumerate(({"FRT_JIT_TILE": "2"}, {"FRT_JIT_TILE": "32"}, {"FRT_JIT_TILE": "32", "FRT_JIT_ORDER": "0"},
-                             {"FRT_JIT_TILE": "64", "FRT_JIT_SUB": "4", "FRT_JIT_ORDER": "2"},
+    for i, env in enumerate(({"FRT_JIT_TILE": "2"}, {"FRT_JIT_TILE": "32", "FRT_JIT_SUB": "0"},
+                             {"FRT_JIT_TILE": "32", "FRT_JIT_ORDER": "0", "FRT_JIT_PART": "17", "FRT_JIT_SUB": "4"},
+                             {"FRT_JIT_TILE": "64", "FRT_JIT_ORDER": "2"},
                              {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"})):
         img, st = _render_env_process(name, env, tmp_path / ("j%d.npy" % i))
         assert st[0] == 1 and st[1] > 0, (env, st)
-        if "FRT_JIT_SUB" in env:
+        if env.get("FRT_JIT_SUB") != "0":
             assert st[2] > 0, (env, st)
         assert np.array_equal(img, ref), env
