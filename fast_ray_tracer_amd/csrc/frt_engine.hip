@@ -513,8 +513,9 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
 
 // the box of the over_points of a tile's path nodes (tile_log2 of them, consecutive lanes of one wave), rounded
 // outward to binary32, for frt_jit_tile (frt_jit_rt.hpp beam_box32); a tile without hits gets an empty box
+// (stbox: the boxes of the tile's sub-tiles of 2^sub_log2 nodes as well, for frt_jit_subtile)
 __device__ __forceinline__ void tile_box(int64_t node, int64_t n, bool hit, const double* op, float* __restrict__ tbox,
-                                         int tile_log2) {
+                                         int tile_log2, float* __restrict__ stbox, int sub_log2) {
     float lo[3], hi[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -522,6 +523,14 @@ __device__ __forceinline__ void tile_box(int64_t node, int64_t n, bool hit, cons
         hi[a] = hit ? __double2float_ru(op[a]) : -__builtin_huge_valf();
     }
     for (int off = 1; off < (1 << tile_log2); off <<= 1) {
+        if (stbox != nullptr && off == (1 << sub_log2) && node < n && (node & (off - 1)) == 0) {
+            float* b = stbox + 6 * (node >> sub_log2);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                b[a] = lo[a];
+                b[a + 3] = hi[a];
+            }
+        }
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             lo[a] = fminf(lo[a], __shfl_xor(lo[a], off, 64));
@@ -542,12 +551,12 @@ template <bool kPat>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPat ? 1 : FRT_PREPARE_WAVES, 8)))
 k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const HitRec* __restrict__ hits,
           NodeCols rec, ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q, unsigned long long* counters,
-          unsigned* err, float* __restrict__ tbox, int tile_log2) {
+          unsigned* err, float* __restrict__ tbox, int tile_log2, float* __restrict__ stbox, int sub_log2) {
     const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double op[3] = {0.0, 0.0, 0.0};
     bool hit = false;
     if (node < n) hit = prepare_node<kPat>(S, B, q, n, hits, rec, heads, next_q, counters, err, node, op);
-    if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2);
+    if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2, stbox, sub_log2);
 }
 
 // one lane per (node, light sample j); lanes of a node are consecutive
@@ -1532,9 +1541,16 @@ struct frt_scene_handle {
     int sub_ps = 0;                    // samples per sub-part slot (frt_jit_sub_ps)
     const int32_t* light_psamp2 = nullptr;  // the sub-parts' samples (frt_jit_light_subparts), -1 padded
     const float* light_sbox = nullptr;      // the sub-parts' boxes (single-row lights), binary32 outward
-    uint32_t* slist = nullptr;         // the node pairs left mixed (input of frt_jit_sub), kMixSegs segments
+    uint32_t* slist = nullptr;         // the tile sub-pairs left mixed (frt_jit_sub's list), kMixSegs segments
     int64_t slist_cap = 0;
     uint64_t sub_pairs = 0, sub_mixed = 0;
+    void* jit_subtile = nullptr;       // sub-tile pair kernel (frt_jit_subtile); null: whole tiles to frt_jit_beam_list
+    int subtile = 0;                   // path nodes per sub-tile (frt_jit_subtile_size) with jit_subtile, else 0
+    float* stbox = nullptr;            // the level's sub-tile boxes (k_prepare): 6 floats per sub-tile
+    int64_t stbox_cap = 0;
+    uint32_t* s2list = nullptr;        // the sub-tile pairs left mixed (frt_jit_subtile's list)
+    int64_t s2list_cap = 0;
+    uint64_t subtile_pairs = 0, subtile_mixed = 0;
     float* tbox = nullptr;             // the level's tile boxes (k_prepare): 6 floats per tile
     int64_t tbox_cap = 0;
     uint32_t* tlist = nullptr;         // undecided (tile, light part) pairs, kMixSegs segments
@@ -2370,6 +2386,8 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             h->tile = fns.tile && fns.list ? frt_jit_tile_size() : 0;
             h->jit_sub = fns.sub;
             h->sub = fns.sub ? frt_jit_sub_count() : 0;
+            h->jit_subtile = fns.subtile;
+            h->subtile = fns.subtile ? frt_jit_subtile_size() : 0;
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
                 void* p = nullptr;
@@ -2577,7 +2595,8 @@ void frt_scene_release(frt_scene_handle* h) {
     if (h->jit_stats) {
         std::vector<unsigned long long> c(kJitStatWords);
         if (hipMemcpy(c.data(), h->jit_stats, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
-            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0, tpairs = 0, tmixed = 0, spairs = 0, smixed = 0;
+            unsigned long long live = 0, amb = 0, pairs = 0, mixed = 0, tpairs = 0, tmixed = 0, spairs = 0, smixed = 0,
+                               upairs = 0, umixed = 0;
             for (int j = 0; j < 64; ++j) {
                 live += c[32 * j];
                 amb += c[32 * j + 1];
@@ -2587,6 +2606,8 @@ void frt_scene_release(frt_scene_handle* h) {
                 tmixed += c[32 * j + 5];
                 spairs += c[32 * j + 6];
                 smixed += c[32 * j + 7];
+                upairs += c[32 * j + 8];
+                umixed += c[32 * j + 9];
             }
             if (tpairs)
                 std::fprintf(stderr, "frt jit stats: tile pair kernel (%d nodes per tile): live tile pairs %llu, mixed %llu (%.2f%%)\n",
@@ -2596,6 +2617,9 @@ void frt_scene_release(frt_scene_handle* h) {
             if (spairs)
                 std::fprintf(stderr, "frt jit stats: sub-part pair kernel (%d sub-parts): live sub-pairs %llu, mixed %llu (%.2f%%)\n",
                              h->sub, spairs, smixed, 100.0 * (double)smixed / (double)spairs);
+            if (upairs)
+                std::fprintf(stderr, "frt jit stats: sub-tile pair kernel (%d nodes per sub-tile): live sub-tile pairs %llu, mixed %llu (%.2f%%)\n",
+                             h->subtile, upairs, umixed, 100.0 * (double)umixed / (double)upairs);
             std::fprintf(stderr, "frt jit stats: live shadow lanes %llu, re-walked in binary64 %llu (%.4f%%)\n", live, amb,
                          live ? 100.0 * (double)amb / (double)live : 0.0);
             std::fprintf(stderr, "frt jit stats: (node, light) pairs: all lit %llu, all shadowed %llu, mixed %llu\n",
@@ -2650,6 +2674,8 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->mixed));
     hip_ignore(hipFree(h->tlist));
     hip_ignore(hipFree(h->slist));
+    hip_ignore(hipFree(h->stbox));
+    hip_ignore(hipFree(h->s2list));
     hip_ignore(hipFree(h->tbox));
     hip_ignore(hipFree(h->err));
     for (hipEvent_t e : h->ev_pool) hip_ignore(hipEventDestroy(e));
@@ -2936,13 +2962,71 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         hipStreamSynchronize(h->stream) != hipSuccess)
                         return;
                     uint64_t listed_s = 0;
-                    list_blocks = seg_table(h->host_mcount, ssegcap, (uint64_t)h->tile, tseg, listed_s);
+                    const bool subtiled = h->jit_subtile && h->subtile > 0 && h->subtile < h->tile && h->stbox;
+                    const uint64_t nst = subtiled ? (uint64_t)(h->tile / h->subtile) : 0;
+                    list_blocks = seg_table(h->host_mcount, ssegcap, subtiled ? nst : (uint64_t)h->tile, tseg, listed_s);
                     h->sub_pairs += listed * (uint64_t)h->sub;
                     h->sub_mixed += listed_s;
                     listed = listed_s;
                     list_in = h->slist;
                     list_segcap = ssegcap;
                     list_boxes = h->light_sbox;
+                    if (subtiled && listed_s > 0) {
+                        // the sub-tile pass: the tile sub-pairs left, per sub-tile of the tile, from its own origin box
+                        const uint64_t tblocks = list_blocks;
+                        const frt::jit::SegTable s1seg = tseg;
+                        const uint32_t s2segcap = (uint32_t)std::max<uint64_t>(
+                            frt::kTraceBlock, ((tblocks + kMixSegs - 1) / kMixSegs) * frt::kTraceBlock);
+                        if (grow(&h->s2list, h->s2list_cap, 2 * (int64_t)s2segcap * kMixSegs)) {  // (out of memory)
+                            (void)hipGetLastError();
+                            h->jit_shadow = nullptr;
+                            hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                            launch_shadow(h, B, rec, n, counts, node0);
+                            return;
+                        }
+                        int stl = 0;
+                        while ((1 << stl) < h->subtile) ++stl;
+                        const float* stb = h->stbox + 6 * (node0 >> stl);
+                        hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
+                        hipError_t ue = hipSuccess;
+                        {
+                            KTimer tu(h, h->cur_st, 14);
+                            const uint64_t max_blocks = ((1ull << 31) - 1) / frt::kTraceBlock;
+                            uint32_t zero = 0;
+                            for (uint64_t b0 = 0; b0 < tblocks && ue == hipSuccess; b0 += max_blocks) {
+                                uint32_t b0u = (uint32_t)b0;
+                                void* uargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&stb, &h->slist, (void*)&s1seg,
+                                                 &b0u, (void*)&ssegcap, &h->light_sbox, &counts, &h->s2list, &h->mcount,
+                                                 (void*)&s2segcap, &h->err, &h->jit_stats};
+                                ue = hipModuleLaunchKernel((hipFunction_t)h->jit_subtile, (unsigned)std::min(max_blocks, tblocks - b0),
+                                                           1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, uargs, nullptr);
+                            }
+                        }
+                        if (ue != hipSuccess) {
+                            std::fprintf(stderr, "frt: scene-specialised sub-tile kernel launch failed (%s); no sub-tiles\n",
+                                         hipGetErrorString(ue));
+                            (void)hipGetLastError();
+                            h->jit_subtile = nullptr;
+                            h->subtile = 0;
+                            hip_ignore(hipMemsetAsync(counts, 0, (size_t)n * h->S.num_lights * sizeof(int32_t), h->stream));
+                            launch_shadow(h, B, rec, n, counts, node0);
+                            return;
+                        }
+                        if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                                           hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                            hipStreamSynchronize(h->stream) != hipSuccess)
+                            return;
+                        uint64_t listed_u = 0;
+                        list_blocks = seg_table(h->host_mcount, s2segcap, (uint64_t)h->subtile, tseg, listed_u);
+                        h->subtile_pairs += listed_s * nst;
+                        h->subtile_mixed += listed_u;
+                        listed = listed_u;
+                        list_in = h->s2list;
+                        list_segcap = s2segcap;
+                    } else if (subtiled) {
+                        list_blocks = 0;
+                        listed = 0;
+                    }
                 } else if (subbed) {
                     list_blocks = 0;  // (no tile pair left)
                     listed = 0;
@@ -2978,7 +3062,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         le = hipModuleLaunchKernel((hipFunction_t)h->jit_list, (unsigned)std::min(max_blocks, list_blocks - b0), 1, 1,
                                                    frt::kTraceBlock, 1, 1, 0, h->stream, largs, nullptr);
                     }
-                    h->node_pairs += listed * (uint64_t)h->tile;
+                    h->node_pairs += listed * (uint64_t)(list_in == h->s2list ? h->subtile : h->tile);
                 } else {
                     uint32_t np = (uint32_t)npairs;
                     const float* no_box = nullptr;
@@ -3722,6 +3806,7 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
     h->rays_walked = 0;
     h->pairs_walked = 0;
     h->tile_pairs = h->tile_mixed = h->node_pairs = h->node_mixed = h->sub_pairs = h->sub_mixed = 0;
+    h->subtile_pairs = h->subtile_mixed = 0;
     const int rc = render_frame(h, P, dev_out, st);
     if (rc) h->gi.built = false;
     return rc;
@@ -3827,9 +3912,14 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 int tl = 0;
                 while (tiles && (1 << tl) < h->tile) ++tl;
                 if (tiles && grow(&h->tbox, h->tbox_cap, 6 * ((n >> tl) + 1))) return -1;
+                const bool subtiles = tiles && h->subtile > 0 && h->subtile < h->tile;
+                int stl = 0;
+                while (subtiles && (1 << stl) < h->subtile) ++stl;
+                if (subtiles && grow(&h->stbox, h->stbox_cap, 6 * ((n >> stl) + 1))) return -1;
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
                                    dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
-                                   L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl);
+                                   L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl,
+                                   subtiles ? h->stbox : nullptr, stl);
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.include_direct && h->samples_per_node > 0) {
@@ -3972,6 +4062,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->shadow_pairs_mixed = h->node_mixed;
         st->shadow_sub_pairs = h->sub_pairs;
         st->shadow_sub_mixed = h->sub_mixed;
+        st->shadow_subtile_pairs = h->subtile_pairs;
+        st->shadow_subtile_mixed = h->subtile_mixed;
         collect_timings(h, st);
     }
 #if defined(FRT_WALK_STATS) || defined(FRT_WALK_PROF)

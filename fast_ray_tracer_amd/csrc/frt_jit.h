@@ -17,6 +17,9 @@ int frt_jit_part_size();
 // the tile pair kernel (frt_jit_tile) decides runs of this many consecutive path nodes at once (a power of two
 // up to 64; 0: off; FRT_JIT_TILE overrides the default 64)
 int frt_jit_tile_size();
+// the sub-tile kernel (frt_jit_subtile, after the sub-part pass) re-decides the tile sub-pairs left mixed for runs of
+// this many of the tile's nodes (a power of two below the tile size; 0: off; FRT_JIT_SUBTILE overrides the default)
+int frt_jit_subtile_size();
 // the sub-part pass (frt_jit_sub, after the tile kernel) splits the parts of the tile pairs left mixed into this many
 // sub-parts (2 ... 32; 0: off; FRT_JIT_SUB overrides the default 16); their sizes, the largest (PS2), and the
 // sub-parts' samples
@@ -39,7 +42,8 @@ struct FrtJitFns {
     void* beam = nullptr;    // frt_jit_beam: every (node, part) pair
     void* tile = nullptr;    // frt_jit_tile: every (tile, part) pair
     void* list = nullptr;    // frt_jit_beam_list: the nodes of the listed tile pairs
-    void* sub = nullptr;     // frt_jit_sub: the sub-parts of the node pairs left mixed
+    void* sub = nullptr;     // frt_jit_sub: the sub-parts of the tile pairs left mixed
+    void* subtile = nullptr; // frt_jit_subtile: the sub-tiles of the tile sub-pairs left mixed
 };
 // compile with hiprtc for `device` (cached per device and source); 0 on success
 int frt_jit_compile(const std::string& src, int device, FrtJitFns& fns, std::string& log);

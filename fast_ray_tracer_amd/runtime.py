@@ -40,11 +40,13 @@ class FrameStats(ctypes.Structure):
                 ("shadow_rays_walked", ctypes.c_uint64), ("shadow_tile_pairs", ctypes.c_uint64),
                 ("shadow_tile_mixed", ctypes.c_uint64), ("shadow_pairs", ctypes.c_uint64),
                 ("shadow_pairs_mixed", ctypes.c_uint64), ("shadow_sub_pairs", ctypes.c_uint64),
-                ("shadow_sub_mixed", ctypes.c_uint64)]
+                ("shadow_sub_mixed", ctypes.c_uint64), ("shadow_subtile_pairs", ctypes.c_uint64),
+                ("shadow_subtile_mixed", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
-        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile", "frt_jit_sub"]
+        subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile", "frt_jit_sub",
+                "frt_jit_subtile"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
@@ -61,6 +63,8 @@ class FrameStats(ctypes.Structure):
             "shadow_tile_pairs": int(self.shadow_tile_pairs), "shadow_tile_mixed": int(self.shadow_tile_mixed),
             "shadow_pairs": int(self.shadow_pairs), "shadow_pairs_mixed": int(self.shadow_pairs_mixed),
             "shadow_sub_pairs": int(self.shadow_sub_pairs), "shadow_sub_mixed": int(self.shadow_sub_mixed),
+            "shadow_subtile_pairs": int(self.shadow_subtile_pairs),
+            "shadow_subtile_mixed": int(self.shadow_subtile_mixed),
         }
 
 

@@ -218,7 +218,8 @@ typedef struct frt_frame_stats {
     int32_t photon_pass;          /* 1: this frame traced its photon maps (a new seed), 0: maps reused / no GI */
     /* kernels inside the slots above (HIP events around each launch on the engine stream):
        0 frt_jit_beam / frt_jit_beam_list (node pair kernel), 1 frt_jit_shadow (per-ray kernel), 2 k_gather_est,
-       3 k_gather_hit, 4 frt_jit_tile (tile pair kernel), 5 frt_jit_sub (sub-part pair kernel) */
+       3 k_gather_hit, 4 frt_jit_tile (tile pair kernel), 5 frt_jit_sub (sub-part pair kernel), 6 frt_jit_subtile
+       (sub-tile pair kernel) */
     double sub_ms[8];
     uint64_t sub_launches[8];
     uint64_t shadow_rays_walked;  /* shadow rays walked one by one; the rest of shadow_rays were resolved
@@ -228,8 +229,10 @@ typedef struct frt_frame_stats {
     uint64_t shadow_tile_mixed;   /* of those, the ones it could not decide (their nodes go to frt_jit_beam_list) */
     uint64_t shadow_pairs;        /* (path node, light part) beams tested by frt_jit_beam / frt_jit_beam_list */
     uint64_t shadow_pairs_mixed;  /* of those, the ones left mixed */
-    uint64_t shadow_sub_pairs;    /* (path node, light sub-part) beams of those mixed pairs tested by frt_jit_sub */
-    uint64_t shadow_sub_mixed;    /* of those, the ones whose rays frt_jit_shadow walked */
+    uint64_t shadow_sub_pairs;    /* (tile, light sub-part) beams of the mixed tile pairs tested by frt_jit_sub */
+    uint64_t shadow_sub_mixed;    /* of those, the ones left mixed */
+    uint64_t shadow_subtile_pairs; /* (sub-tile, light sub-part) beams of those tested by frt_jit_subtile */
+    uint64_t shadow_subtile_mixed; /* of those, the ones whose nodes frt_jit_beam_list tested */
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for b in "$@"; do
-    timeout -k 10 240 python -u bench.py --steps 4 --warmup 1 --gi-steps 0 --no-cpu-baseline --no-render-multi \
+    timeout -k 10 240 python -u bench.py --steps 4 --warmup 1 --gi-steps 0 --no-cpu-baseline --no-render-multi --no-scaling-proxy \
         --batch-samples $b > gpurun_out/ab_batch_$b.json 2> gpurun_out/ab_batch_$b.err || exit $?
     python3 -c "
 import json,sys; d=json.loads(open('gpurun_out/ab_batch_$b.json').read().strip().splitlines()[-1])
