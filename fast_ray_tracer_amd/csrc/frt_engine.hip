@@ -612,6 +612,9 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow_redo(DevScene S, Batch B
 #ifndef FRT_SHADE_FACTOR
 #define FRT_SHADE_FACTOR 1
 #endif
+#ifndef FRT_SHADE_ALG
+#define FRT_SHADE_ALG 1
+#endif
 // lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725): the
 // A, D, S triples of path node i into out (out[4k + c]: term k, channel c)
 __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, const NodeRec& nr, int64_t i,
@@ -642,6 +645,18 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     constexpr bool kFactored = FRT_SHADE_FACTOR != 0;
                     double sum_ldn = 0.0, sum_b = 0.0, sum_fb = 0.0;
                     const double cdist = (nr.Ns + 2) * 0.5 * k1Pi;
+                    // The light vector and the half vector by their shared terms (FRT_SHADE_ALG, default 1): with
+                    // v = p - over_point, m2 = v.v and r = 1/|v|, lightv = v r, so lightv.n = (v.n) r and
+                    // lightv.e = (v.e) r; the half vector h = (lightv + e) / |lightv + e| has |lightv + e|^2 =
+                    // lightv.lightv + 2 lightv.e + e.e, and n.h, e.h, lightv.h are (n.lightv + n.e) / |..|,
+                    // (lightv.e + e.e) / |..|, (lightv.lightv + lightv.e) / |..|: two dot products and a few
+                    // multiplies per point instead of the normalised vectors and five dot products (a few ulps
+                    // from vector_normalize's path, like the reciprocal estimates; ned = n.e is the node's).
+                    // FRT_SHADE_ALG=0 builds: the vectors as the reference forms them (A/B runs).
+                    constexpr bool kAlg = FRT_SHADE_ALG != 0;
+                    const double ee = dot3(nr.eyev, nr.eyev);
+                    // pow_ns's exponent test once per node (the same Ns for every point)
+                    const double nsd = nr.Ns;
                     // (the next point's load is issued before this point's arithmetic, so its latency hides
                     // behind the ~700 cycles of binary64 work instead of stalling every iteration)
                     auto points = [&](const double* pts) {
@@ -654,9 +669,15 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                             nx[1] = q[1];
                             nx[2] = q[2];
                             double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
-                            double lv[3];
-                            normalize3_shade(diff, lv);
-                            double ldn = dot3(lv, nr.normalv);
+                            double lv[3] = {0.0, 0.0, 0.0}, ldn, m2 = 0.0, rl = 0.0;
+                            if (kAlg) {
+                                m2 = dot3(diff, diff);
+                                rl = rsqrt_shade(m2);
+                                ldn = dot3(diff, nr.normalv) * rl;
+                            } else {
+                                normalize3_shade(diff, lv);
+                                ldn = dot3(lv, nr.normalv);
+                            }
                             if (S.cfg.include_diffuse && ldn >= 0.0) {
                                 if (kFactored) {
                                     sum_ldn += ldn;
@@ -669,13 +690,24 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                                 }
                             }
                             if (S.cfg.include_spec_highlight && ldn >= 0.0) {
-                                double ndl = dot3(nr.normalv, lv);
-                                double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
-                                normalize3_shade(tmp, hv);
-                                double ndh = fmax(0.0, dot3(nr.normalv, hv));
-                                double edh_inv = recip_shade(fmax(0.0, dot3(nr.eyev, hv)));
-                                double ldh = dot3(lv, hv);
-                                double dist_term = kFactored ? pow_ns(ndh, nr.Ns) * cdist
+                                double ndl, ndh, edh, ldh;
+                                if (kAlg) {
+                                    ndl = ldn;
+                                    const double el = dot3(diff, nr.eyev) * rl, ll = (m2 * rl) * rl;
+                                    const double rh = rsqrt_shade(ll + 2.0 * el + ee);
+                                    ndh = fmax(0.0, (ldn + ned) * rh);
+                                    edh = fmax(0.0, (el + ee) * rh);
+                                    ldh = (ll + el) * rh;
+                                } else {
+                                    ndl = dot3(nr.normalv, lv);
+                                    double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
+                                    normalize3_shade(tmp, hv);
+                                    ndh = fmax(0.0, dot3(nr.normalv, hv));
+                                    edh = fmax(0.0, dot3(nr.eyev, hv));
+                                    ldh = dot3(lv, hv);
+                                }
+                                const double edh_inv = recip_shade(edh);
+                                double dist_term = kFactored ? pow_ns(ndh, nsd) * cdist
                                                              : (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
                                 double gc = 2.0 * ndh * edh_inv;
                                 double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
@@ -3822,7 +3854,11 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
     const int64_t npix = nrows * hs;
     const int32_t spp = (int32_t)(h->S.cam.usteps * h->S.cam.vsteps);
     if (spp <= 0) return fail("render: usteps*vsteps must be positive");
-    int64_t batch = P->batch_samples > 0 ? P->batch_samples : (int64_t)1 << 23;  // 8 M samples: tools/ab_batch.sh (2 M 219.6, 4 M 212.4, 8 M 208.4, 16 M 207.8 ms headline)
+    // 128 M samples (the whole headline frame: about 55 GB of level state on a 288 GB device): each batch pays the
+    // shadow pass's host round trips (the list counts that size its next launch) and every level's, so fewer,
+    // larger batches leave the device idle less often (tools/ab_batch.sh, round 4: 8 M 54.3, 32 M 49.1,
+    // 128 M 48.0 ms headline; round 2, with a slower shadow pass: 2 M 219.6, 8 M 208.4, 16 M 207.8)
+    int64_t batch = P->batch_samples > 0 ? P->batch_samples : (int64_t)1 << 27;
     int64_t pix_per_batch = std::max<int64_t>(1, batch / spp);
     const int path = h->S.cfg.path_length;
     if (st) {

@@ -117,16 +117,22 @@ __device__ __forceinline__ double rcp_nr(double y) {
     for (int k = 0; k < FRT_SHADE_NEWTON; ++k) r = __builtin_fma(r, __builtin_fma(-y, r, 1.0), r);
     return r;
 }
+// 1 / sqrt(m2) with the IEEE operations where the estimate's steps may leave range. (The slow paths below sit
+// behind a wave-uniform branch: the compiler would otherwise if-convert them and every lane would pay for the
+// IEEE division in every light point.)
+__device__ __forceinline__ double rsqrt_shade(double m2) {
+    if (!FRT_SHADE_FAST) return 1.0 / sqrt(m2);
+    double inv = rsqrt_nr(m2);
+    const bool slow = !shade_in_range(m2);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) inv = 1.0 / sqrt(m2);
+    }
+    return inv;
+}
 // vector_normalize (linalg.c:141-148) with the approximate reciprocal magnitude
 __device__ __forceinline__ void normalize3_shade(const double* v, double* r) {
     const double m2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-    double inv;
-    if (FRT_SHADE_FAST) {
-        inv = rsqrt_nr(m2);
-        if (!shade_in_range(m2)) inv = 1.0 / sqrt(m2);  // (divergent: only where some lane needs it)
-    } else {
-        inv = 1.0 / sqrt(m2);
-    }
+    const double inv = rsqrt_shade(m2);
     r[0] = v[0] * inv;
     r[1] = v[1] * inv;
     r[2] = v[2] * inv;
@@ -135,13 +141,19 @@ __device__ __forceinline__ void normalize3_shade(const double* v, double* r) {
 __device__ __forceinline__ double recip_shade(double y) {
     if (!FRT_SHADE_FAST) return 1.0 / y;
     double r = rcp_nr(y);
-    if (!shade_in_range(y)) r = 1.0 / y;
+    const bool slow = !shade_in_range(y);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) r = 1.0 / y;
+    }
     return r;
 }
 __device__ __forceinline__ double div_shade(double a, double b) {
     if (!FRT_SHADE_FAST) return a / b;
     double q = a * rcp_nr(b);
-    if (!(shade_in_range(b) && (a == 0.0 || shade_in_range(a)))) q = a / b;
+    const bool slow = !(shade_in_range(b) && (a == 0.0 || shade_in_range(a)));
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) q = a / b;
+    }
     return q;
 }
 
