@@ -344,7 +344,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gi-steps", type=int, default=1, help="timed GI frames (0: skip the GI line)")
     ap.add_argument("--scene", default=DEFAULT_SCENE)
-    ap.add_argument("--batch-samples", type=int, default=0)
+    # camera samples per batch on the resident handle: the whole headline frame (frt_render_params.batch_samples; the
+    # engine's own default, 2^23, suits one-shot calls such as render_multi, which allocate per call: DESIGN.md §2)
+    ap.add_argument("--batch-samples", type=int, default=1 << 27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-render-multi", action="store_true", help="skip the drop-in entry point timing")
     ap.add_argument("--no-scaling-proxy", action="store_true", help="skip the one-GPU proxy of the N-rank split")
@@ -539,7 +541,7 @@ def main():
                      "8x8 CMJ" if args.scene == DEFAULT_SCENE
                      else "reference codegen main.c: tests/golden/scenes/%s.c" % args.scene),
             "config": {"workload": args.scene, "width": W, "height": H, "spp": scene.spp,
-                       "path_length": 5, "parallelism": "rows%d" % world},
+                       "path_length": 5, "parallelism": "rows%d" % world, "batch_samples": args.batch_samples},
             "rays_per_frame_traced": total_rays / args.steps,
             # rays walked one by one (primary + secondary + the shadow rays of the pairs the pair kernels could
             # not decide): `value` counts every shadow ray, also those decided for a whole beam at once

@@ -3854,11 +3854,16 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
     const int64_t npix = nrows * hs;
     const int32_t spp = (int32_t)(h->S.cam.usteps * h->S.cam.vsteps);
     if (spp <= 0) return fail("render: usteps*vsteps must be positive");
-    // 128 M samples (the whole headline frame: about 55 GB of level state on a 288 GB device): each batch pays the
-    // shadow pass's host round trips (the list counts that size its next launch) and every level's, so fewer,
-    // larger batches leave the device idle less often (tools/ab_batch.sh, round 4: 8 M 54.3, 32 M 49.1,
-    // 128 M 48.0 ms headline; round 2, with a slower shadow pass: 2 M 219.6, 8 M 208.4, 16 M 207.8)
-    int64_t batch = P->batch_samples > 0 ? P->batch_samples : (int64_t)1 << 27;
+    // 8 M samples unless the caller asks for more. Each batch pays the shadow pass's host round trips (the list
+    // counts that size its next launch) and every level's, so a handle that renders frame after frame takes the
+    // whole frame in one batch (frt_render_params.batch_samples; bench.py: 2^27 = the headline frame, about
+    // 70 GB of level state, 8 M / 32 M / 128 M samples per batch gave 54.3 / 49.1 / 48.0 ms headline frames,
+    // tools/ab_batch.sh). The default suits one-shot calls (render_multi): a handle's first frame allocates its
+    // level state, and the driver clears fresh device memory at ~11 GB/s, 6 s for 128 M samples
+    // (tools/rm_batch.py, profiles/r04_ab_batch.txt). FRT_BATCH_SAMPLES overrides the default (A/B runs).
+    const char* benv = std::getenv("FRT_BATCH_SAMPLES");
+    const int64_t bdef = benv && std::atoll(benv) > 0 ? (int64_t)std::atoll(benv) : (int64_t)1 << 23;
+    int64_t batch = P->batch_samples > 0 ? P->batch_samples : bdef;
     int64_t pix_per_batch = std::max<int64_t>(1, batch / spp);
     const int path = h->S.cfg.path_length;
     if (st) {
