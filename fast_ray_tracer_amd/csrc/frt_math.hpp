@@ -304,9 +304,15 @@ __device__ __forceinline__ double pow_ns(double x, double y) {
         const unsigned e0 = (unsigned)__builtin_amdgcn_readfirstlane((int)e);
         if (__ballot(e != e0) == 0ull) {
             // one exponent in the whole wave (one material's Ns): a scalar loop over its bits, the same
-            // products in the same order as below, without the selects and the squarings past the top bit
+            // products in the same order as below, without the selects, the first product (1 x b is exact)
+            // and the squaring past the top bit
+            bool first = true;
             for (unsigned k = 0; (e0 >> k) != 0u; ++k) {
-                if ((e0 >> k) & 1u) r = r * b;
+                if ((e0 >> k) & 1u) {
+                    r = first ? b : r * b;
+                    first = false;
+                }
+                if ((e0 >> (k + 1)) == 0u) break;
                 b *= b;
             }
             return r;

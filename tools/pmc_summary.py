@@ -15,7 +15,7 @@ import re
 import sys
 
 out, kre, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-res = {"kernel": kre, "workload": workload}
+res = {"kernel": sys.argv[4] if len(sys.argv) > 4 else kre, "workload": workload}
 for f in glob.glob(out + "/kt/**/*kernel_stats.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         if re.search(kre, row["Name"]):
