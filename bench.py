@@ -60,6 +60,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_GINST_S = 1024 * 2.4 / 2.0
 # SALU issue peak: one scalar unit per CU, one instruction per cycle, shared by the CU's 4 SIMDs
 SALU_PEAK_GINST_S = 256 * 2.4
+# binary64 vector peak (MI355X spec, 78.6 TFLOP/s): 1024 SIMDs x 16 lanes per cycle x 2 flops (FMA) at 2.4 GHz
+# (profiles/r01_microbench_valu.txt measures ~5 SIMD-cycles per wave64 f64 FMA against the 4 of this figure)
+FP64_PEAK_TFLOPS = 78.6
 
 # algorithmic HBM bytes of the shadow kernel ("byte model"), reported by the engine per frame
 # as stats.shadow_kernel_bytes: per shaded path node the 64-byte ShadowHead it reads (over_point, key,
@@ -174,7 +177,8 @@ def latest_pmc(kernel: str, workload: str):
             t = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if t.get("kernel") == kernel and t.get("workload") == workload:
+        # (older summaries name the kernel by the regex their pass used, "k_shadow<")
+        if t.get("kernel", "").rstrip("<") == kernel and t.get("workload") == workload:
             best = (p, t)
     return best
 
@@ -245,12 +249,70 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
         pairs_per_launch = (d.get("shadow_pairs") or 0) / nb
         roof.setdefault("issue", {})[bname] = dict(issue_block(fb[1], bavg, pairs_per_launch, "pairs"),
                                                    avg_launch_ms=round(bavg, 4), source=os.path.relpath(fb[0], ROOT))
-    nt = d.get("sub_launches", {}).get("frt_jit_tile")
-    ft = latest_pmc("frt_jit_tile", workload)
-    if nt and ft:
-        tavg = d["sub_ms"]["frt_jit_tile"] / nt
-        roof.setdefault("issue", {})["frt_jit_tile"] = dict(issue_block(ft[1], tavg, d["shadow_tile_pairs"] / nt, "tile_pairs"),
-                                                            avg_launch_ms=round(tavg, 4), source=os.path.relpath(ft[0], ROOT))
+    for kn, units, uname in (("frt_jit_tile", d.get("shadow_tile_pairs"), "tile_pairs"),
+                             ("frt_jit_sub", d.get("shadow_sub_pairs"), "tile_sub_pairs"),
+                             ("frt_jit_subtile", d.get("shadow_subtile_pairs"), "subtile_pairs")):
+        nt = d.get("sub_launches", {}).get(kn)
+        ft = latest_pmc(kn, workload)
+        if nt and ft:
+            tavg = d["sub_ms"][kn] / nt
+            roof.setdefault("issue", {})[kn] = dict(issue_block(ft[1], tavg, (units or 0) / nt, uname),
+                                                    avg_launch_ms=round(tavg, 4), source=os.path.relpath(ft[0], ROOT))
+    return roof
+
+
+def frame_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> dict:
+    """The frame's dominant kernel by live time (HIP events around its launches in the stats frame: the engine's
+    sub-timers for the scene-specialised shadow kernels and k_shade_lit, its per-slot timers for k_trace (level
+    0), k_prepare and k_combine_resolve), with the bound its committed PMC pass on the same workload shows:
+      * "valu-fp64" (k_shade_lit, k_trace): achieved = the pass's binary64 FLOPs per launch (64 x (ADD + MUL +
+        TRANS) + 128 x FMA wave-instructions) over the live launch time, against the 78.6 TFLOP/s binary64
+        vector peak; `issue` adds the VALU / SALU issue rates;
+      * "valu-issue" (the pair and per-ray shadow kernels): the issue rates as `roofline_shadow_pass` gives them;
+      * "hbm" otherwise: FETCH_SIZE + WRITE_SIZE per launch over the live launch time against 8 TB/s.
+    `traffic` is FETCH_SIZE + WRITE_SIZE per launch of the same PMC run in every case."""
+    subs, sl = d.get("sub_ms", {}), d.get("sub_launches", {})
+    cands = {}
+    for k in ("k_shade_lit", "frt_jit_beam", "frt_jit_shadow", "frt_jit_tile", "frt_jit_sub", "frt_jit_subtile"):
+        if sl.get(k):
+            cands[k] = (subs[k], sl[k])
+    slots = [("k_trace", "trace_primary"), ("k_prepare", "prepare"), ("k_combine_resolve", "resolve")]
+    if not d.get("shadow_jit"):
+        slots.append(("k_shadow", "shadow"))  # (the generic walk: scenes the generator does not take)
+    for k, slot in slots:
+        if launches.get(slot):
+            cands[k] = (kernel_ms[slot], launches[slot])
+    if not cands:
+        return {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    dom = max(cands, key=lambda k: cands[k][0])
+    ms, nl = cands[dom]
+    pname = "frt_jit_beam_list" if dom == "frt_jit_beam" and d.get("shadow_tile_pairs") else dom
+    avg = ms / nl
+    roof = {"kernel": pname, "avg_launch_ms": round(avg, 4), "launches_per_frame": nl, "ms_per_frame": round(ms, 3),
+            "timing": "HIP events around each launch on the engine stream (frt_frame_stats)",
+            "candidates_ms_per_frame": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])}}
+    found = latest_pmc(pname, workload)
+    t = found[1] if found else {}
+    traffic = (t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)) if found else None
+    f64 = [t.get("SQ_INSTS_VALU_%s_F64_per_launch" % x) for x in ("ADD", "MUL", "FMA", "TRANS")]
+    if found and all(v is not None for v in f64):
+        flops = 64.0 * (f64[0] + f64[1] + f64[3]) + 128.0 * f64[2]
+        ach = flops / (avg * 1e-3) / 1e12
+        roof.update({"bound": "valu-fp64", "achieved": round(ach, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_launch": round(flops)})
+    elif pname.startswith("frt_jit"):
+        roof.update({"bound": "valu-issue", "achieved": None, "peak": None, "unit": None, "frac": None,
+                     "note": "instruction-issue bound; see roofline_shadow_pass.issue for the VALU / SALU fractions"})
+    else:
+        ach = traffic / (avg * 1e-3) / 1e9 if traffic else None
+        roof.update({"bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None})
+    roof["traffic"] = round(traffic) if traffic else None
+    if found:
+        roof["source"] = os.path.relpath(found[0], ROOT)
+        roof["issue"] = issue_block(t, avg, 1.0, "launch")
+        if "rocprof_avg_ms" in t:
+            roof["rocprof_avg_launch_ms"] = round(t["rocprof_avg_ms"], 4)
     return roof
 
 
@@ -518,13 +580,8 @@ def main():
         ms_per_step = 1e3 * t_max / args.steps
         value = total_rays / t_max / 1e6
         ref_rays = reference_rays(args.scene)
-        dom = max(kernel_ms, key=kernel_ms.get)
-        if dom == "shadow":
-            roof = shadow_roofline(d, kernel_ms, launches, args.scene)
-        else:
-            roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                    "traffic": None, "kernel": dom,
-                    "avg_launch_ms": round(kernel_ms[dom] / max(1, launches[dom]), 4)}
+        roof = frame_roofline(d, kernel_ms, launches, args.scene)
+        roof_shadow = shadow_roofline(d, kernel_ms, launches, args.scene) if launches.get("shadow") else None
         out = {
             "metric": "Mrays/s (primary+shadow+secondary) + wall-clock/frame, 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -553,21 +610,25 @@ def main():
             "sub_ms_per_frame": {k: round(v, 4) for k, v in d.get("sub_ms", {}).items()},
             "shadow_pass": {
                 "kernels_ms_per_frame": {k: round(v, 4) for k, v in d.get("sub_ms", {}).items()
-                                         if k in ("frt_jit_beam", "frt_jit_shadow", "frt_jit_tile")},
+                                         if k.startswith("frt_jit_")},
                 "shadow_rays_per_frame": d["shadow_rays"],
                 "shadow_rays_walked_per_ray": d.get("shadow_rays_walked"),
                 "tile_pairs": d.get("shadow_tile_pairs"), "tile_pairs_mixed": d.get("shadow_tile_mixed"),
+                "tile_sub_pairs": d.get("shadow_sub_pairs"), "tile_sub_pairs_mixed": d.get("shadow_sub_mixed"),
+                "subtile_pairs": d.get("shadow_subtile_pairs"), "subtile_pairs_mixed": d.get("shadow_subtile_mixed"),
                 "node_pairs": d.get("shadow_pairs"), "node_pairs_mixed": d.get("shadow_pairs_mixed"),
                 # the fraction of all shadow rays walked one by one (those of the (node, light part) pairs left
                 # mixed after the tile and node pair kernels)
                 "rays_walked_frac": (round(d["shadow_rays_walked"] / d["shadow_rays"], 4)
                                      if d.get("shadow_rays") else None),
                 "note": "every shadow ray's occlusion is computed exactly (bit-identical to a per-ray walk, "
-                        "tests/test_jit.py); frt_jit_tile resolves (tile of consecutive path nodes, light part) "
-                        "beams, frt_jit_beam (frt_jit_beam_list after the tile kernel; one timer) the (path node, "
-                        "light part) pairs of the tiles left, by interval bounds over all their rays; frt_jit_shadow "
-                        "walks the rays of the pairs left"},
+                        "tests/test_jit.py) by a hierarchy of beams: frt_jit_tile (64 consecutive path nodes, 16-sample "
+                        "light part), frt_jit_sub (the tile pairs left, per light sample), frt_jit_subtile (the tile "
+                        "sample pairs left, per 16-node sub-tile), frt_jit_beam (frt_jit_beam_list: the nodes of the "
+                        "sub-tile pairs left), each deciding its beam by interval bounds over all its rays; "
+                        "frt_jit_shadow walks the rays left one by one (DESIGN.md 3.3)"},
             "roofline": roof,
+            "roofline_shadow_pass": roof_shadow,
         }
         out.update(rm)
         if gi is not None:

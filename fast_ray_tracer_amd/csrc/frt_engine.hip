@@ -3999,9 +3999,11 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 else
                     hipLaunchKernelGGL(k_shade<false>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
                                        L.counts, L.surface, split ? h->shade_lit : nullptr, h->shade_lcount, segcap);
-                if (split)
+                if (split) {
+                    KTimer tl(h, st, 15);  // (inside the shade slot: k_shade_lit alone, sub_ms[7])
                     hipLaunchKernelGGL(k_shade_lit, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec,
                                        L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap);
+                }
                 FRT_HIP(hipGetLastError());
             }
             if (h->S.cfg.use_gi) {

@@ -46,7 +46,7 @@ class FrameStats(ctypes.Structure):
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
         subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile", "frt_jit_sub",
-                "frt_jit_subtile"]
+                "frt_jit_subtile", "k_shade_lit"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),

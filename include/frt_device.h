@@ -219,7 +219,7 @@ typedef struct frt_frame_stats {
     /* kernels inside the slots above (HIP events around each launch on the engine stream):
        0 frt_jit_beam / frt_jit_beam_list (node pair kernel), 1 frt_jit_shadow (per-ray kernel), 2 k_gather_est,
        3 k_gather_hit, 4 frt_jit_tile (tile pair kernel), 5 frt_jit_sub (sub-part pair kernel), 6 frt_jit_subtile
-       (sub-tile pair kernel) */
+       (sub-tile pair kernel), 7 k_shade_lit (the shading of the path nodes some light reaches) */
     double sub_ms[8];
     uint64_t sub_launches[8];
     uint64_t shadow_rays_walked;  /* shadow rays walked one by one; the rest of shadow_rays were resolved
