@@ -45,6 +45,7 @@
 #include "frt_shade.hpp"
 #include "frt_shadow.hpp"
 #include "frt_jit_rt.hpp"
+#include "frt_camera.hpp"
 #include "frt_cols.hpp"
 
 namespace frt {
@@ -171,147 +172,15 @@ struct NodeCols {
 };
 
 
-struct QueuedRay {
-    double o[3];
-    double d[3];
-    uint64_t key;
-    int32_t parent;
-    int32_t slot;
-};
+
 
 // k*Spawned: the child ray was queued (its k_combine writes the parent's slot; otherwise the slot reads as 0)
 enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8, kReflSpawned = 16, kRefrSpawned = 32 };
 
 
 
-// ---- stochastic camera sampling (counter-based RNG; the reference draws drand48) ----
-// Uniform double in [0, 1) for draw d of stream (seed, key): 53 bits of a splitmix64 hash.
-__device__ __forceinline__ double rng_uniform(uint64_t seed, uint64_t key, uint64_t d) {
-    const uint64_t h = mix64(seed ^ mix64(key * 0x9e3779b97f4a7c15ULL + d * 0xd1b54a32d192ed03ULL + 0x632be59bd9b4e019ULL));
-    return (double)(h >> 11) * 0x1.0p-53;
-}
 
-// Jittered correlated multi-jittered sub-pixel point (u, v) of one pixel: the
-// reference's sampler_reset_2d (sampler.c:411-470: canonical pattern with a
-// drand48 jitter per cell, then the x rows and y columns shuffled with
-// drand48) evaluated for one cell by tracing the two shuffles backwards.
-// Draw numbering: canonical cell (j, i) -> x: 2(jV+i), y: 2(jV+i)+1;
-// x-row shuffle step j -> 2UV + j; y-column shuffle step i -> 2UV + V + i.
-__device__ inline void cmj_point(uint64_t seed, uint64_t pixel, int U, int V, int u, int v, double* out) {
-    const uint64_t base = 2ull * (uint64_t)U * (uint64_t)V;
-    // x: rows j < V of length U are permuted (sampler.c:442-450, n = steps[1] = V, m = steps[0] = U)
-    int p = v;
-    for (int j = V - 1; j >= 0; --j) {
-        const int k = (int)(j + rng_uniform(seed, pixel, base + j) * (double)(V - j));
-        if (p == j) p = k;
-        else if (p == k) p = j;
-    }
-    {
-        const int f = p * U + u;           // flat index of the source cell
-        const int jj = f / V, ii = f % V;  // canonical layout idx = j * V + i (sampler.c:419-427)
-        const double r = rng_uniform(seed, pixel, 2ull * (uint64_t)f);
-        out[0] = (ii + (jj + r) / (double)U) / (double)V;
-    }
-    // y: columns i < U are permuted (sampler.c:452-460)
-    p = u;
-    for (int i = U - 1; i >= 0; --i) {
-        const int k = (int)(i + rng_uniform(seed, pixel, base + (uint64_t)V + i) * (double)(U - i));
-        if (p == i) p = k;
-        else if (p == k) p = i;
-    }
-    {
-        const int f = v * U + p;
-        const int jj = f / V, ii = f % V;
-        const double r = rng_uniform(seed, pixel, 2ull * (uint64_t)f + 1);
-        out[1] = (jj + (ii + r) / (double)V) / (double)U;
-    }
-}
 
-// aperture_fn (camera.c:11-82): rejection sampling on [0,1)^2; point-like types give the centre
-__device__ inline void aperture_point(const frt_camera& cam, uint64_t seed, uint64_t sample, double* xy,
-                                      unsigned& err) {
-    const double* a = cam.aperture_args;
-    const int type = cam.aperture_type;
-    if (type == 6 || type == 4 || type == 5 || type == 8 || type < 0 || type > 8) {  // point / not-implemented types
-        xy[0] = 0.5;
-        xy[1] = 0.5;
-        return;
-    }
-    for (int attempt = 0; attempt < 4096; ++attempt) {
-        const double x = rng_uniform(seed ^ 0xa5e7u, sample, 2ull * attempt);
-        const double y = rng_uniform(seed ^ 0xa5e7u, sample, 2ull * attempt + 1);
-        const double u = 2 * x - 1, v = 2 * y - 1;
-        bool ok;
-        switch (type) {
-        case 0: ok = !(u * u + v * v > a[0]); break;                                    // circle r1
-        case 1: ok = ((u > a[0]) && (u <= a[1])) || ((v > a[2]) && (v <= a[3])); break;  // cross x1 x2 y1 y2
-        case 2:                                                                           // diamond b1..b4
-            ok = (u <= 0) ? (-u + a[0] <= v) && (v < u + a[1]) : (0 <= x) ? (u + a[2] <= v) && (v < -u + a[3]) : false;
-            break;
-        case 3: {  // doughnut r1 r2
-            const double mag = u * u + v * v;
-            ok = !(mag > a[0] || mag < a[1]);
-            break;
-        }
-        default: ok = true; break;  // square
-        }
-        if (ok) {
-            xy[0] = x;
-            xy[1] = y;
-            return;
-        }
-    }
-    err |= kErrAperture;  // the reference would loop forever
-    xy[0] = 0.5;
-    xy[1] = 0.5;
-}
-
-__device__ __forceinline__ void ray_for_pixel(const frt_camera& cam, double px, double py, const double* jit,
-                                              const double* ap, Ray& r) {
-    // renderer.c:95-129; ap = aperture_fn's point in [0,1)^2 (sample_aperture subtracts 0.5, camera.c:85-90)
-    double xoff = (px + jit[0]) * cam.pixel_size;
-    double yoff = (py + jit[1]) * cam.pixel_size;
-    double wx = cam.half_width - xoff, wy = cam.half_height - yoff;
-    double p[3] = {wx, wy, -cam.canvas_distance}, pixel[3], origin[3];
-    xf_point(cam.inv, p, pixel);
-    double q[3] = {(ap[0] - 0.5) * cam.aperture_size, (ap[1] - 0.5) * cam.aperture_size, 0.0};
-    xf_point(cam.inv, q, origin);
-    double v[3] = {pixel[0] - origin[0], pixel[1] - origin[1], pixel[2] - origin[2]};
-    r.o[0] = origin[0];
-    r.o[1] = origin[1];
-    r.o[2] = origin[2];
-    normalize3(v, r.d);
-}
-
-// camera ray of sample s of a batch (k_trace level 0 and k_prepare level 0)
-__device__ __forceinline__ void camera_ray(const DevScene& S, const Batch& B, int64_t s, Ray& r, uint64_t& key,
-                                           unsigned& err) {
-    const int64_t pix = B.pixel_begin + s / B.spp;
-    const int sub = (int)(s % B.spp);  // sub = v * usteps + u
-    const int64_t hs = S.cam.hsize;
-    const int64_t row = B.row_begin + (pix / hs) * B.row_stride;
-    const int64_t col = pix % hs;
-    const uint64_t global_pixel = (uint64_t)(row * hs + col);
-    const uint64_t global_sample = global_pixel * (uint64_t)B.spp + (uint64_t)sub;
-    double jit[2], ap[2] = {0.5, 0.5};
-    if (S.cam.jitter) {
-        const int U = (int)S.cam.usteps, V = (int)S.cam.vsteps;
-        cmj_point(B.seed, global_pixel, U, V, sub % U, sub / U, jit);
-    } else {
-        jit[0] = S.sample_table[2 * sub];
-        jit[1] = S.sample_table[2 * sub + 1];
-    }
-    if (S.cam.aperture_size != 0.0) aperture_point(S.cam, B.seed, global_sample, ap, err);
-    ray_for_pixel(S.cam, (double)col, (double)row, jit, ap, r);
-    key = (global_sample << 12) | 1ull;
-}
-
-struct HitRec {
-    double t;
-    int32_t node;  // -1: miss
-    int32_t pad;
-    double n1, n2;  // refractive indices either side of the hit (containers)
-};
 
 extern __shared__ __align__(16) char frt_walk_smem[];
 
@@ -347,6 +216,42 @@ __attribute__((amdgpu_waves_per_eu((kFeat & kFeatTorus) ? 1 : FRT_TRACE_WAVES, 8
     double n12[2];
     const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12, filter_casts != 0);
     if (i < n) hits[i] = live ? HitRec{t, node, 0, n12[0], n12[1]} : HitRec{0.0, -1, 0, 1.0, 1.0};
+    if (e) atomicOr(err, e);
+}
+
+// the rays frt_jit_trace (frt_jit.hip) could not settle in binary32: the generic walk, grid-stride over the list
+// (whole waves per step, as k_shadow_redo)
+template <int kFeat>
+__global__ void __launch_bounds__(kTraceBlock) k_trace_redo(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
+                                                            HitRec* __restrict__ hits, unsigned* err,
+                                                            const int32_t* __restrict__ redo,
+                                                            const unsigned* __restrict__ redo_count, unsigned redo_cap) {
+    const unsigned cnt = min(*redo_count, redo_cap);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned e = 0;
+    for (int64_t base = wave * 64; base < (int64_t)cnt; base += nwaves * 64) {
+        const int64_t k = base + (threadIdx.x & 63);
+        const int64_t i = k < (int64_t)cnt ? (int64_t)redo[k] : -1;
+        const bool live = i >= 0 && i < n;
+        Ray r{{0, 0, 0}, {0, 0, 1}};
+        if (live) {
+            if (q == nullptr) {
+                uint64_t key;
+                camera_ray(S, B, i, r, key, e);
+            } else {
+                const QueuedRay& qr = q[queue_slot(B, i)];
+                for (int a = 0; a < 3; ++a) {
+                    r.o[a] = qr.o[a];
+                    r.d[a] = qr.d[a];
+                }
+            }
+        }
+        double t;
+        double n12[2];
+        const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12, false);
+        if (live) hits[i] = HitRec{t, node, 0, n12[0], n12[1]};
+    }
     if (e) atomicOr(err, e);
 }
 
@@ -1577,6 +1482,9 @@ struct frt_scene_handle {
     int64_t slist_cap = 0;
     uint64_t sub_pairs = 0, sub_mixed = 0;
     void* jit_subtile = nullptr;       // sub-tile pair kernel (frt_jit_subtile); null: whole tiles to frt_jit_beam_list
+    void* jit_trace = nullptr;         // closest-hit kernel (frt_jit_trace); null: k_trace for every ray
+    int32_t* tredo = nullptr;          // rays frt_jit_trace hands to the generic walk (k_trace_redo), + counter
+    int64_t tredo_cap = 0;
     int subtile = 0;                   // path nodes per sub-tile (frt_jit_subtile_size) with jit_subtile, else 0
     float* stbox = nullptr;            // the level's sub-tile boxes (k_prepare): 6 floats per sub-tile
     int64_t stbox_cap = 0;
@@ -2419,6 +2327,8 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             h->jit_sub = fns.sub;
             h->sub = fns.sub ? frt_jit_sub_count() : 0;
             h->jit_subtile = fns.subtile;
+            // (the closest-hit kernel writes n1 = n2 = 1: scenes with refractive indices other than one keep k_trace)
+            h->jit_trace = sc->config.all_ni_one ? fns.trace : nullptr;
             h->subtile = fns.subtile ? frt_jit_subtile_size() : 0;
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
@@ -2708,6 +2618,7 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->slist));
     hip_ignore(hipFree(h->stbox));
     hip_ignore(hipFree(h->s2list));
+    hip_ignore(hipFree(h->tredo));
     hip_ignore(hipFree(h->tbox));
     hip_ignore(hipFree(h->err));
     for (hipEvent_t e : h->ev_pool) hip_ignore(hipEventDestroy(e));
@@ -2823,9 +2734,50 @@ static void launch_trace_f(frt_scene_handle* h, const frt::Batch& B, const frt::
                        h->stream, h->S, B, q, n, hits, h->err, filter_casts);
 }
 
+template <int F>
+static void launch_trace_redo_f(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
+                                frt::HitRec* hits) {
+    const unsigned cap = (unsigned)(h->tredo_cap - 2);  // (the list, then its counter)
+    hipLaunchKernelGGL(frt::k_trace_redo<F>, dim3(1024), dim3(frt::kTraceBlock), h->lds_bytes, h->stream, h->S, B, q, n,
+                       hits, h->err, h->tredo, (const unsigned*)(h->tredo + cap), cap);
+}
+
 static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
                          frt::HitRec* hits = nullptr, int filter_casts = 0) {
     if (hits == nullptr) hits = h->hits;
+    // the scene-specialised closest hit (frt_jit_trace), its undecided rays to the generic walk (k_trace_redo)
+    static const bool jit_trace_env = !(std::getenv("FRT_JIT_TRACE") && std::atoi(std::getenv("FRT_JIT_TRACE")) == 0);
+    if (h->jit_trace && jit_trace_env && !filter_casts && n > 0 && n < ((int64_t)1 << 31)) {
+        if (!grow(&h->tredo, h->tredo_cap, n + 2)) {  // (a list of every ray at worst, then its counter)
+            unsigned cap = (unsigned)(h->tredo_cap - 2);
+            unsigned* cnt = (unsigned*)(h->tredo + cap);
+            hip_ignore(hipMemsetAsync(cnt, 0, sizeof(unsigned), h->stream));
+            void* args[] = {&h->S, (void*)&B, (void*)&q, &n, &hits, &h->err, &h->tredo, &cnt, &cap};
+            if (hipModuleLaunchKernel((hipFunction_t)h->jit_trace, (unsigned)grid_for(n, frt::kTraceBlock), 1, 1,
+                                      frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr) == hipSuccess) {
+                switch (h->S.features & 3) {
+                case 0: launch_trace_redo_f<0>(h, B, q, n, hits); break;
+                case 1: launch_trace_redo_f<1>(h, B, q, n, hits); break;
+                case 2: launch_trace_redo_f<2>(h, B, q, n, hits); break;
+                default: launch_trace_redo_f<3>(h, B, q, n, hits); break;
+                }
+                static const bool trace_stats = std::getenv("FRT_JIT_TRACE_STATS") != nullptr;
+                if (trace_stats) {  // (debug: the undecided share per launch; synchronises)
+                    unsigned c = 0;
+                    hip_ignore(hipMemcpyAsync(&c, cnt, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+                    hip_ignore(hipStreamSynchronize(h->stream));
+                    std::fprintf(stderr, "frt: frt_jit_trace level %d: %lld rays, %u to the generic walk\n", B.level,
+                                 (long long)n, c);
+                }
+                return;
+            }
+            std::fprintf(stderr, "frt: scene-specialised closest-hit kernel launch failed; k_trace\n");
+            (void)hipGetLastError();
+            h->jit_trace = nullptr;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     switch (h->S.features & 3) {
     case 0: launch_trace_f<0>(h, B, q, n, hits, filter_casts); break;
     case 1: launch_trace_f<1>(h, B, q, n, hits, filter_casts); break;

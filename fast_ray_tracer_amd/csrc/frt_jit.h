@@ -44,6 +44,7 @@ struct FrtJitFns {
     void* list = nullptr;    // frt_jit_beam_list: the nodes of the listed tile pairs
     void* sub = nullptr;     // frt_jit_sub: the sub-parts of the tile pairs left mixed
     void* subtile = nullptr; // frt_jit_subtile: the sub-tiles of the tile sub-pairs left mixed
+    void* trace = nullptr;   // frt_jit_trace: closest hit per ray (null where the scene has none)
 };
 // compile with hiprtc for `device` (cached per device and source); 0 on success
 int frt_jit_compile(const std::string& src, int device, FrtJitFns& fns, std::string& log);

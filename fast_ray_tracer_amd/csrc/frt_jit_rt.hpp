@@ -237,6 +237,21 @@ __device__ __forceinline__ bool ray32v(const double* lp, const double* op, World
 
 __device__ __forceinline__ bool ray32(const Lane32& L, World32& w, Iv& dist) { return ray32v(L.lp, L.op, w, dist); }
 
+// (frt_jit_trace) a closest-hit ray in binary32: o~ = f32(o) as above, d~ = f32(d), within u of the reference's
+// binary64 direction, inside the 6.6u the model above allows the world ray, for a direction of unit length
+// (camera, reflected and refracted rays); false when that does not hold within 1e-6 or a value is not finite:
+// the lane takes the generic walk
+__device__ __forceinline__ bool ray32d(const Ray& r, World32& w) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w.o[a] = (float)r.o[a];
+        w.d[a] = (float)r.d[a];
+    }
+    world32_finish(w);
+    const double n2 = r.d[0] * r.d[0] + r.d[1] * r.d[1] + r.d[2] * r.d[2];
+    return n2 > 1.0 - 1e-6 && n2 < 1.0 + 1e-6 && w.omax <= 0x1p100f;  // (false for NaN)
+}
+
 // the reference's binary64 ray, exactly as shadow_lane computes it. Every lane of a wave runs the
 // blocks that call this (uniform branches), so lanes without a ray (padding, nodes without a hit)
 // get a placeholder instead of reading through their null light point.
@@ -1028,6 +1043,38 @@ __device__ __forceinline__ void cube_top32_beam(const Node32& nd, const BW& w, c
 }
 
 // sorted entries of a non-cube leaf inside a CSG unit, exactly (binary64 ray of its parent frame)
+// (frt_jit_trace) a leaf's first smallest positive entry in emission order, exactly (binary64), as an interval:
+// ok false when it has none
+template <int kType, bool kXf>
+__device__ __forceinline__ void leaf_first_pos(const DevScene& S, const WalkNode& nd, const Ray& R, bool act, Iv& t,
+                                               int& j, bool& ok) {
+    const Ray lr = kXf ? xf_ray_walk(nd.m, R) : R;
+    LeafHits H;
+    leaf_hits<true>(kType, S.prim + nd.prim, lr, H);
+    ok = false;
+    j = 0;
+    double best = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double x = H.t.at(k);
+        if (k < H.t.n && x > 0 && (!ok || x < best)) {
+            best = x;
+            j = k;
+            ok = true;
+        }
+    }
+    ok = ok && act;
+    t = iv_of(best);
+}
+// (frt_jit_trace) entry j of a leaf, exactly as the generic walk computes it
+template <int kType, bool kXf>
+__device__ __forceinline__ double leaf_entry(const DevScene& S, const WalkNode& nd, const Ray& R, int j) {
+    const Ray lr = kXf ? xf_ray_walk(nd.m, R) : R;
+    LeafHits H;
+    leaf_hits<true>(kType, S.prim + nd.prim, lr, H);
+    return H.t.at(j);
+}
+
 template <int kType, bool kXf>
 __device__ __forceinline__ void leaf_slots_iv(const DevScene& S, const WalkNode& nd, const Ray& R, bool act, Iv& t0,
                                               Iv& t1, bool& v0, bool& v1) {

@@ -158,3 +158,17 @@ def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
         if env.get("FRT_JIT_SUB") != "0":
             assert st[2] > 0, (env, st)
         assert np.array_equal(img, ref), env
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "checkered_torus_120", "checkered_cylinder_120", "group_test_150x50",
+                                  "teapot_low_100", "checkered_sphere_dof_100", "patterns_160x80", "cornell_gi_16",
+                                  "test_scene_120", "bump_map_100"])
+def test_jit_closest_hit_equals_generic_walk(built, name, tmp_path):
+    """The scene-specialised closest-hit kernel (frt_jit_trace: binary32 intervals, the winner's t from its own leaf
+    in binary64, the rays it cannot settle handed to the generic walk by k_trace_redo) against k_trace for every
+    ray (FRT_JIT_TRACE=0): the canvases are bit-identical (camera rays, reflected rays and, on cornell_gi_16,
+    final-gather rays)."""
+    ref, _ = _render_env_process(name, {"FRT_JIT_TRACE": "0"}, tmp_path / "g.npy")
+    img, _ = _render_env_process(name, {}, tmp_path / "j.npy")
+    assert np.array_equal(img, ref), name
