@@ -73,9 +73,12 @@ static_assert(sizeof(NodeRec) == 216, "NodeRec layout");
 // node's ShadowHead (which k_prepare writes for the shadow pass anyway: no second copy), and its material
 // colours (13 words), which k_prepare stores only for materials with patterns on them (kOwnColors; every
 // other reader takes them from the material table): the colours of pattern-free materials are never
-// written or read per node, and a missed ray writes only its material / parent / slot words.
+// written or read per node, and a missed ray writes only its material / parent / slot words. Words that a
+// node's flags or its level make constant are not written either: parent / slot at level 0 (-1, 0), over_d
+// unless a pattern sets it (kOwnD; else the material's 1 - Tr, as prepare computes it), the Schlick factor
+// unless kMix (else 0).
 struct NodeCore {
-    int32_t material, parent, slot, flags;
+    int32_t material, flags, parent, slot;
     double normalv[3], eyev[3];
     double over_d, rf;
 };
@@ -84,12 +87,15 @@ struct NodeColors {
     double Ns;
 };
 static_assert(sizeof(NodeCore) == 80 && sizeof(NodeColors) == 104, "NodeCols layout");
-enum : int32_t { kOwnColors = 64 };  // (NodeFlags bit) the node's colours are in NodeCols::col
+// k*Spawned: the child ray was queued (its k_combine writes the parent's slot; otherwise the slot reads as 0)
+enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8, kReflSpawned = 16, kRefrSpawned = 32 };
+enum : int32_t { kOwnColors = 64, kOwnD = 128 };  // (NodeFlags bits) the node's colours / over_d are in NodeCols
 
 struct NodeCols {
     Cols<NodeCore> core;
     Cols<NodeColors> col;
     const ShadowHead* head = nullptr;  // over_point, key (the level's ShadowHead array)
+    int32_t root = 0;                  // level 0: parent / slot are -1 / 0 and not stored
     static size_t bytes(int64_t cap) { return Cols<NodeCore>::bytes(cap) + Cols<NodeColors>::bytes(cap); }
     void set(uint64_t* base, int64_t cap) {  // (host) one allocation of bytes(cap)
         core.w = base;
@@ -97,7 +103,7 @@ struct NodeCols {
         col.w = base + (size_t)Cols<NodeCore>::kWords * cap;
         col.cap = cap;
     }
-    __device__ __forceinline__ void store(int64_t i, const NodeRec& v, bool own_colors) const {
+    __device__ __forceinline__ void store(int64_t i, const NodeRec& v, bool own_colors, bool own_d) const {
         NodeCore c;
         for (int k = 0; k < 3; ++k) {
             c.normalv[k] = v.normalv[k];
@@ -106,10 +112,18 @@ struct NodeCols {
         c.material = v.material;
         c.parent = v.parent;
         c.slot = v.slot;
-        c.flags = v.flags | (own_colors ? kOwnColors : 0);
+        c.flags = v.flags | (own_colors ? kOwnColors : 0) | (own_d ? kOwnD : 0);
         c.over_d = v.over_d;
         c.rf = v.rf;
-        core.store(i, c);
+        uint64_t t[10];
+        __builtin_memcpy(t, &c, sizeof(c));
+        const int64_t cap = core.cap;
+        core.w[i] = t[0];
+        if (!root) core.w[cap + i] = t[1];
+#pragma unroll
+        for (int f = 2; f < 8; ++f) core.w[f * cap + i] = t[f];
+        if (own_d) core.w[8 * cap + i] = t[8];
+        if (c.flags & kMix) core.w[9 * cap + i] = t[9];
         if (own_colors) {
             NodeColors o;
             for (int k = 0; k < 3; ++k) {
@@ -124,13 +138,24 @@ struct NodeCols {
     }
     // a missed ray: material -1 with its parent and slot (the words k_combine reads)
     __device__ __forceinline__ void store_miss(int64_t i, int32_t parent, int32_t slot) const {
-        const uint64_t w4 = (uint64_t)(uint32_t)-1 | ((uint64_t)(uint32_t)parent << 32);
-        const uint64_t w5 = (uint64_t)(uint32_t)slot;
-        core.w[0 * core.cap + i] = w4;
-        core.w[1 * core.cap + i] = w5;
+        core.w[i] = (uint64_t)(uint32_t)-1;  // (flags 0)
+        if (!root) core.w[core.cap + i] = (uint64_t)(uint32_t)parent | ((uint64_t)(uint32_t)slot << 32);
     }
     __device__ __forceinline__ NodeRec load(int64_t i, const frt_material* __restrict__ mats) const {
-        const NodeCore c = core.load(i);
+        uint64_t t[10];
+        const int64_t cap = core.cap;
+        t[0] = core.w[i];
+        t[1] = root ? (uint64_t)(uint32_t)-1 : core.w[cap + i];
+#pragma unroll
+        for (int f = 2; f < 8; ++f) t[f] = core.w[f * cap + i];
+        const int32_t mat = (int32_t)(uint32_t)t[0], fl = (int32_t)(t[0] >> 32);
+        const double od = (fl & kOwnD) ? __longlong_as_double((long long)core.w[8 * cap + i])
+                          : mat >= 0 ? 1.0 - mats[mat].Tr : 0.0;
+        const double rf = (fl & kMix) ? __longlong_as_double((long long)core.w[9 * cap + i]) : 0.0;
+        t[8] = (uint64_t)__double_as_longlong(od);
+        t[9] = (uint64_t)__double_as_longlong(rf);
+        NodeCore c;
+        __builtin_memcpy(&c, t, sizeof(c));
         NodeRec v;
         const ShadowHead& hd = head[i];  // (dead, and not loaded, where a kernel uses neither field)
         for (int k = 0; k < 3; ++k) {
@@ -174,8 +199,6 @@ struct NodeCols {
 
 
 
-// k*Spawned: the child ray was queued (its k_combine writes the parent's slot; otherwise the slot reads as 0)
-enum NodeFlags : int32_t { kReflApplies = 1, kRefrApplies = 2, kMix = 4, kDissolve = 8, kReflSpawned = 16, kRefrSpawned = 32 };
 
 
 
@@ -404,7 +427,7 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
     PSTAMP(3);
     // the colours per node only where a pattern makes them vary (prepare: map_Ka / Kd / Ks / refl / Ns)
     const bool own = kPat && (M.map_Ka >= 0 || M.map_Kd >= 0 || M.map_Ks >= 0 || M.map_refl >= 0 || M.map_Ns >= 0);
-    rec.store(node, nr, own);
+    rec.store(node, nr, own, kPat && M.map_d >= 0);
     ShadowHead hd;
     for (int k = 0; k < 3; ++k) hd.over_point[k] = c.over_point[k];
     hd.key = key;
@@ -2287,6 +2310,16 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             casts[(size_t)i] = (m >= 0 && m < sc->num_materials && sc->materials[m].casts_shadow) ? 1 : 0;
         }
         S.casts = upload(h, casts.data(), casts.size(), rc);
+        // per node: its transform chain root-most first (frt_traverse.hpp xf_chain), n = -1 past three
+        std::vector<int4> xchain((size_t)std::max(1, sc->num_nodes), make_int4(0, 0, 0, 0));
+        for (int i = 0; i < sc->num_nodes; ++i) {
+            int ids[64], n = 0;
+            for (int x = sc->nodes[i].xform >= 0 ? i : sc->nodes[i].tparent; x >= 0 && n < 64; x = sc->nodes[x].tparent)
+                ids[n++] = sc->nodes[x].xform;
+            if (n <= 3) xchain[(size_t)i] = make_int4(n, n > 0 ? ids[n - 1] : 0, n > 1 ? ids[n - 2] : 0, n > 2 ? ids[n - 3] : 0);
+            else xchain[(size_t)i] = make_int4(-1, 0, 0, 0);
+        }
+        S.xchain = upload(h, xchain.data(), xchain.size(), rc);
     }
     if (rc) {
         frt_scene_release(h);
@@ -2648,6 +2681,7 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
         void* p = nullptr;
         FRT_HIP(hipMalloc(&p, frt::NodeCols::bytes(nc)));
         L.rec.set((uint64_t*)p, nc);
+        L.rec.root = d == 0 ? 1 : 0;
     }
     FRT_HIP(hipMalloc((void**)&L.head, nc * sizeof(frt::ShadowHead)));
     L.rec.head = L.head;

@@ -20,6 +20,24 @@ __device__ __forceinline__ int first_xf(const DevScene& S, int leaf) {
 // (a perturbed pattern's point, see pattern_at_shape), so no transform adds its translation
 __device__ inline void world_to_object(const DevScene& S, int leaf, const double* p, double* out, bool w0 = false) {
     double q[3] = {p[0], p[1], p[2]};
+    const int4 c = xf_chain(S, leaf);
+    if (c.x >= 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k < c.x) {
+                double t[3];
+                if (w0) xf_vector(xform_of(S, xf_chain_id(c, k)), q, t);
+                else xf_point(xform_of(S, xf_chain_id(c, k)), q, t);
+                q[0] = t[0];
+                q[1] = t[1];
+                q[2] = t[2];
+            }
+        }
+        out[0] = q[0];
+        out[1] = q[1];
+        out[2] = q[2];
+        return;
+    }
     const int first = first_xf(S, leaf);
     int n = 0;
     for (int x = first; x >= 0; x = S.nodes[x].tparent) n++;
@@ -41,6 +59,18 @@ __device__ inline void world_to_object(const DevScene& S, int leaf, const double
 // shape_normal_to_world (shapes.c:92-114): leaf-most transform first, each one
 // followed by a normalize; identity levels copy without normalizing
 __device__ inline void normal_to_world(const DevScene& S, int leaf, double* n) {
+    const int4 c = xf_chain(S, leaf);
+    if (c.x >= 0) {
+#pragma unroll
+        for (int k = 2; k >= 0; --k) {
+            if (k < c.x) {
+                double t[3];
+                xf_normal_t(xform_of(S, xf_chain_id(c, k)), n, t);
+                normalize3(t, n);
+            }
+        }
+        return;
+    }
     for (int x = first_xf(S, leaf); x >= 0; x = S.nodes[x].tparent) {
         double t[3];
         xf_normal_t(xform_of(S, S.nodes[x].xform), n, t);

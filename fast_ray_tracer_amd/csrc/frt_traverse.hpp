@@ -139,6 +139,7 @@ struct DevScene {
     const double* __restrict__ light_points;
     const double* __restrict__ sample_table;
     const uint8_t* __restrict__ casts;  // per node: material casts shadows (leaves)
+    const int4* __restrict__ xchain;    // per node: {n, ids}: its transform chain, root-most first (xf_chain)
     int32_t num_nodes, num_roots, num_lights, num_patterns;
     // per-lane LDS capacities of the walk (computed from the tree at upload)
     int32_t list_cap;    // CSG list entries
@@ -940,9 +941,23 @@ __device__ int walk(const DevScene& S, const Ray& world, double distance, bool l
     return kShadow ? result : best;
 }
 
+// a node's transform chain (its own transform, then its transformed ancestors' through the tparent links):
+// {n, the xform ids root-most first} for chains of up to three, n = -1 for deeper ones (the links then). One
+// 16-byte load instead of the links' dependent loads (built at upload, frt_engine.hip)
+__device__ __forceinline__ int4 xf_chain(const DevScene& S, int leaf) { return S.xchain[leaf]; }
+__device__ __forceinline__ int xf_chain_id(const int4& c, int k) { return k == 0 ? c.y : k == 1 ? c.z : c.w; }
+
 // recompute a leaf's local ray (through every transformed ancestor, root first,
 // exactly as the walk composed it) — used to recover triangle (u, v)
 __device__ inline Ray leaf_local_ray(const DevScene& S, int leaf, const Ray& world) {
+    const int4 c = xf_chain(S, leaf);
+    if (c.x >= 0) {
+        Ray r = world;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (k < c.x) r = xf_ray(xform_of(S, xf_chain_id(c, k)), r);
+        return r;
+    }
     const int first = S.nodes[leaf].xform >= 0 ? leaf : S.nodes[leaf].tparent;
     int n = 0;
     for (int x = first; x >= 0; x = S.nodes[x].tparent) n++;
