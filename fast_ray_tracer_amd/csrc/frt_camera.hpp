@@ -17,11 +17,12 @@ struct QueuedRay {
 };
 
 // a ray's closest hit (k_trace -> k_prepare)
+// (the refractive indices either side of a hit, from the containers, go to an array of their own (n12, two per
+// ray), written only where a scene has indices other than one: most scenes write and read 16 bytes per hit)
 struct HitRec {
     double t;
     int32_t node;  // -1: miss
     int32_t pad;
-    double n1, n2;  // refractive indices either side of the hit (containers)
 };
 
 // ---- stochastic camera sampling (counter-based RNG; the reference draws drand48) ----

@@ -216,7 +216,8 @@ extern __shared__ __align__(16) char frt_walk_smem[];
 template <int kFeat>
 __global__ void __launch_bounds__(kTraceBlock)
 __attribute__((amdgpu_waves_per_eu((kFeat & kFeatTorus) ? 1 : FRT_TRACE_WAVES, 8))) k_trace(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n,
-                                                       HitRec* __restrict__ hits, unsigned* err, int filter_casts) {
+                                                       HitRec* __restrict__ hits, double* __restrict__ hn12, unsigned* err,
+                                                       int filter_casts) {
     // every lane of the wave takes part in the (wave-coherent) walk; queued rays with
     // parent < -1 are placeholders (final-gather slots of nodes without a gather)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -238,7 +239,13 @@ __attribute__((amdgpu_waves_per_eu((kFeat & kFeatTorus) ? 1 : FRT_TRACE_WAVES, 8
     double t;
     double n12[2];
     const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12, filter_casts != 0);
-    if (i < n) hits[i] = live ? HitRec{t, node, 0, n12[0], n12[1]} : HitRec{0.0, -1, 0, 1.0, 1.0};
+    if (i < n) {
+        hits[i] = live ? HitRec{t, node, 0} : HitRec{0.0, -1, 0};
+        if (hn12 != nullptr) {
+            hn12[2 * i] = live ? n12[0] : 1.0;
+            hn12[2 * i + 1] = live ? n12[1] : 1.0;
+        }
+    }
     if (e) atomicOr(err, e);
 }
 
@@ -273,7 +280,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_redo(DevScene S, Batch B,
         double t;
         double n12[2];
         const int node = walk<false, kFeat>(S, r, 0.0, live, t, frt_walk_smem, e, n12, false);
-        if (live) hits[i] = HitRec{t, node, 0, n12[0], n12[1]};
+        if (live) hits[i] = HitRec{t, node, 0};  // (every refractive index is one where this runs: no n12)
     }
     if (e) atomicOr(err, e);
 }
@@ -285,7 +292,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace_redo(DevScene S, Batch B,
 // (one path node; returns whether it has a hit, its over_point in op)
 template <bool kPat>
 __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, const QueuedRay* __restrict__ q,
-                                             int64_t n, const HitRec* __restrict__ hits, NodeCols& rec,
+                                             int64_t n, const HitRec* __restrict__ hits, const double* __restrict__ hn12,
+                                             NodeCols& rec,
                                              ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q,
                                              unsigned long long* counters, unsigned* err, int64_t node, double* op) {
     // this block's counter line: next-level queue segment count (word level + 1), pruned (16), hits (17)
@@ -329,8 +337,8 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
     Hit h{hr.t, -1, -1, hr.node};
     Comps c;
     prepare<kPat>(S, r, h, c);
-    c.n1 = hr.n1;
-    c.n2 = hr.n2;
+    c.n1 = hn12 != nullptr ? hn12[2 * node] : 1.0;
+    c.n2 = hn12 != nullptr ? hn12[2 * node + 1] : 1.0;
     PSTAMP(2);
     wave_count(line + 17, true);  // shaded path nodes
     const frt_material& M = S.materials[c.material];
@@ -478,12 +486,13 @@ __device__ __forceinline__ void tile_box(int64_t node, int64_t n, bool hit, cons
 template <bool kPat>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPat ? 1 : FRT_PREPARE_WAVES, 8)))
 k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const HitRec* __restrict__ hits,
+          const double* __restrict__ hn12,
           NodeCols rec, ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q, unsigned long long* counters,
           unsigned* err, float* __restrict__ tbox, int tile_log2, float* __restrict__ stbox, int sub_log2) {
     const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double op[3] = {0.0, 0.0, 0.0};
     bool hit = false;
-    if (node < n) hit = prepare_node<kPat>(S, B, q, n, hits, rec, heads, next_q, counters, err, node, op);
+    if (node < n) hit = prepare_node<kPat>(S, B, q, n, hits, hn12, rec, heads, next_q, counters, err, node, op);
     if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2, stbox, sub_log2);
 }
 
@@ -1032,6 +1041,7 @@ template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed, int map, int depth,
                                                        const QueuedRay* __restrict__ q, const double* __restrict__ power,
                                                        int64_t n, const HitRec* __restrict__ hits,
+                                                       const double* __restrict__ hn12,
                                                        QueuedRay* __restrict__ next_q, double* __restrict__ next_power,
                                                        unsigned long long* next_count, int64_t next_cap,
                                                        StoredPhoton* __restrict__ store, unsigned long long* store_count,
@@ -1051,8 +1061,8 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint64_t seed
     Hit h{hr.t, -1, -1, hr.node};
     Comps c;
     prepare<kPat>(S, r, h, c);
-    c.n1 = hr.n1;
-    c.n2 = hr.n2;
+    c.n1 = hn12 != nullptr ? hn12[2 * i] : 1.0;
+    c.n2 = hn12 != nullptr ? hn12[2 * i + 1] : 1.0;
     const frt_material& M = S.materials[c.material];
     const bool had_diffuse = (qr.slot & 1) != 0, had_specular = (qr.slot & 2) != 0;
     const uint64_t e = qr.key;
@@ -1555,6 +1565,8 @@ struct frt_scene_handle {
     std::vector<Level> levels;
     frt::HitRec* hits = nullptr;  // closest hits of the level being traced
     int64_t hits_cap = 0;
+    double* hn12 = nullptr;  // the refractive indices of the level's hits (scenes with indices other than one)
+    int64_t hn12_cap = 0;
     frt::Cols<frt::Tri9> sample_col;
     int64_t sample_cap = 0;
     double* out_dev = nullptr;
@@ -1583,6 +1595,8 @@ struct frt_scene_handle {
         int64_t pq_cap[2] = {0, 0}, ppow_cap[2] = {0, 0};
         frt::HitRec* phits = nullptr;
         int64_t phits_cap = 0;
+        double* pn12 = nullptr;  // (as hn12, for the photons' hits)
+        int64_t pn12_cap = 0;
         frt::StoredPhoton* store = nullptr;
         int64_t store_cap = 0;
         frt::QueuedRay* gq = nullptr;
@@ -2624,6 +2638,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(L.qprefix));
     }
     hip_ignore(hipFree(h->hits));
+    hip_ignore(hipFree(h->hn12));
     {
         auto& G = h->gi;
         for (int m = 0; m < 2; ++m) {
@@ -2632,6 +2647,7 @@ void frt_scene_release(frt_scene_handle* h) {
             hip_ignore(hipFree(G.ppow[m]));
         }
         hip_ignore(hipFree(G.phits));
+        hip_ignore(hipFree(G.pn12));
         hip_ignore(hipFree(G.store));
         hip_ignore(hipFree(G.gq));
         hip_ignore(hipFree(G.ghits));
@@ -2763,9 +2779,9 @@ static void collect_timings(frt_scene_handle* h, frt_frame_stats* st) {
 // frames / the quartic keeps register pressure down for scenes that lack them
 template <int F>
 static void launch_trace_f(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
-                           frt::HitRec* hits, int filter_casts) {
+                           frt::HitRec* hits, int filter_casts, double* hn12) {
     hipLaunchKernelGGL(frt::k_trace<F>, dim3(grid_for(n, frt::kTraceBlock)), dim3(frt::kTraceBlock), h->lds_bytes,
-                       h->stream, h->S, B, q, n, hits, h->err, filter_casts);
+                       h->stream, h->S, B, q, n, hits, hn12, h->err, filter_casts);
 }
 
 template <int F>
@@ -2776,12 +2792,13 @@ static void launch_trace_redo_f(frt_scene_handle* h, const frt::Batch& B, const 
                        hits, h->err, h->tredo, (const unsigned*)(h->tredo + cap), cap);
 }
 
+// hn12: where the hits' refractive indices go (null: every index is one, or nobody reads them)
 static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
-                         frt::HitRec* hits = nullptr, int filter_casts = 0) {
+                         frt::HitRec* hits = nullptr, int filter_casts = 0, double* hn12 = nullptr) {
     if (hits == nullptr) hits = h->hits;
     // the scene-specialised closest hit (frt_jit_trace), its undecided rays to the generic walk (k_trace_redo)
     static const bool jit_trace_env = !(std::getenv("FRT_JIT_TRACE") && std::atoi(std::getenv("FRT_JIT_TRACE")) == 0);
-    if (h->jit_trace && jit_trace_env && !filter_casts && n > 0 && n < ((int64_t)1 << 31)) {
+    if (h->jit_trace && jit_trace_env && !filter_casts && hn12 == nullptr && n > 0 && n < ((int64_t)1 << 31)) {
         if (!grow(&h->tredo, h->tredo_cap, n + 2)) {  // (a list of every ray at worst, then its counter)
             unsigned cap = (unsigned)(h->tredo_cap - 2);
             unsigned* cnt = (unsigned*)(h->tredo + cap);
@@ -2813,10 +2830,10 @@ static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::Qu
         }
     }
     switch (h->S.features & 3) {
-    case 0: launch_trace_f<0>(h, B, q, n, hits, filter_casts); break;
-    case 1: launch_trace_f<1>(h, B, q, n, hits, filter_casts); break;
-    case 2: launch_trace_f<2>(h, B, q, n, hits, filter_casts); break;
-    default: launch_trace_f<3>(h, B, q, n, hits, filter_casts); break;
+    case 0: launch_trace_f<0>(h, B, q, n, hits, filter_casts, hn12); break;
+    case 1: launch_trace_f<1>(h, B, q, n, hits, filter_casts, hn12); break;
+    case 2: launch_trace_f<2>(h, B, q, n, hits, filter_casts, hn12); break;
+    default: launch_trace_f<3>(h, B, q, n, hits, filter_casts, hn12); break;
     }
 }
 
@@ -3257,8 +3274,10 @@ static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t
         const int64_t store_cap = batch * (int64_t)std::min(path, 16);
         if (grow(&G.pq[0], G.pq_cap[0], batch) || grow(&G.pq[1], G.pq_cap[1], batch) ||
             grow(&G.ppow[0], G.ppow_cap[0], 3 * batch) || grow(&G.ppow[1], G.ppow_cap[1], 3 * batch) ||
-            grow(&G.phits, G.phits_cap, batch) || grow(&G.store, G.store_cap, store_cap))
+            grow(&G.phits, G.phits_cap, batch) || grow(&G.store, G.store_cap, store_cap) ||
+            (!h->S.cfg.all_ni_one && grow(&G.pn12, G.pn12_cap, 2 * batch)))
             return -1;
+        double* pn12 = h->S.cfg.all_ni_one ? nullptr : G.pn12;
         unsigned long long* store_count = h->counters + 24;
         unsigned long long* next_count = h->counters + 25;
         FRT_HIP(hipMemsetAsync(h->counters + 24, 0, 2 * sizeof(unsigned long long), h->stream));
@@ -3269,10 +3288,10 @@ static int trace_light_photons(frt_scene_handle* h, int map, int light, uint64_t
         int cur = 0;
         for (int depth = 0; depth < path && n > 0; ++depth) {
             FRT_HIP(hipMemsetAsync(next_count, 0, sizeof(unsigned long long), h->stream));
-            launch_trace(h, B, G.pq[cur], n, G.phits, 1);
+            launch_trace(h, B, G.pq[cur], n, G.phits, 1, pn12);
             FRT_HIP(hipGetLastError());
             hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_photon_hit<true> : k_photon_hit<false>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, lseed, map, depth,
-                               G.pq[cur], G.ppow[cur], n, G.phits, G.pq[cur ^ 1], G.ppow[cur ^ 1], next_count,
+                               G.pq[cur], G.ppow[cur], n, G.phits, pn12, G.pq[cur ^ 1], G.ppow[cur ^ 1], next_count,
                                batch, G.store, store_count, store_cap, h->err);
             FRT_HIP(hipGetLastError());
             unsigned long long nn = 0;
@@ -3925,10 +3944,12 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             B.next_segcap = N.cap / kQueueSegs;
             FRT_HIP(hipMemsetAsync(L.counts, 0, (size_t)n * std::max(1, h->S.num_lights) * sizeof(int32_t), h->stream));
             if (grow(&h->hits, h->hits_cap, n)) return -1;
+            if (!h->S.cfg.all_ni_one && grow(&h->hn12, h->hn12_cap, 2 * n)) return -1;
+            double* hn12 = h->S.cfg.all_ni_one ? nullptr : h->hn12;
             const QueuedRay* q = d == 0 ? nullptr : L.q;
             {
                 KTimer t(h, st, d == 0 ? 5 : 0);
-                launch_trace(h, B, q, n);
+                launch_trace(h, B, q, n, h->hits, 0, hn12);
                 FRT_HIP(hipGetLastError());
             }
             {
@@ -3944,7 +3965,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 while (subtiles && (1 << stl) < h->subtile) ++stl;
                 if (subtiles && grow(&h->stbox, h->stbox_cap, 6 * ((n >> stl) + 1))) return -1;
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
-                                   dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits,
+                                   dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits, hn12,
                                    L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl,
                                    subtiles ? h->stbox : nullptr, stl);
                 FRT_HIP(hipGetLastError());
