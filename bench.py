@@ -358,13 +358,15 @@ def gather_roofline(gd: dict) -> dict:
     return roof
 
 
-def scaling_proxy(renderer, shard, height: int, frame_ms_1: float, ns=(2, 4, 8), reps: int = 2, seed_of=None) -> dict:
+def scaling_proxy(renderer, shard, height: int, frame_ms_1: float, ns=(2, 4, 8), reps: int = 2, seed_of=None,
+                  batch_samples: int = 0) -> dict:
     """The multi-GPU split measured on this one GPU: for N ranks, rank r renders rows r, r + N, ... (the
     interleave of dist.py / render_multi); ranks 0 and N - 1 (the first and last row sets) are timed on their
     own, the best of `reps` runs each, and the predicted efficiency is frame_ms_1 / (N x the slower rank).
     What it leaves out: the canvas gather over RCCL (66 MB per 1920x1080 frame over xGMI, ~1 ms) and any
     interference between GPUs. seed_of(n, r, i): a seed per run (the GI workload: a photon pass in every run,
-    as every rank of a real run traces its own maps)."""
+    as every rank of a real run traces its own maps). batch_samples: the timed frames' own (a rank of the real run
+    renders its rows with the same setting)."""
     import torch
     out = {}
     for n in ns:
@@ -375,7 +377,8 @@ def scaling_proxy(renderer, shard, height: int, frame_ms_1: float, ns=(2, 4, 8),
                 seed = seed_of(n, r, i) if seed_of else 0x5EED
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                renderer.render_into(shard.data_ptr(), row_begin=r, row_end=height, row_stride=n, seed=seed)
+                renderer.render_into(shard.data_ptr(), row_begin=r, row_end=height, row_stride=n, seed=seed,
+                                     batch_samples=batch_samples)
                 torch.cuda.synchronize()
                 t = 1e3 * (time.perf_counter() - t0)
                 best = t if best is None else min(best, t)
@@ -409,6 +412,9 @@ def main():
     # camera samples per batch on the resident handle: the whole headline frame (frt_render_params.batch_samples; the
     # engine's own default, 2^23, suits one-shot calls such as render_multi, which allocate per call: DESIGN.md §2)
     ap.add_argument("--batch-samples", type=int, default=1 << 27)
+    # the GI frame runs on a handle of its own without an untimed warmup frame, so its level state is allocated
+    # inside the timed frame: 2^23 samples per batch (a whole-frame batch allocates ~5 s of driver-cleared memory)
+    ap.add_argument("--gi-batch-samples", type=int, default=1 << 23)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-render-multi", action="store_true", help="skip the drop-in entry point timing")
     ap.add_argument("--no-scaling-proxy", action="store_true", help="skip the one-GPU proxy of the N-rank split")
@@ -489,9 +495,10 @@ def main():
     cap = shard_capacity(world, H)
     shard = torch.zeros((cap, W, 4), dtype=torch.float64, device="cuda")
 
-    def frame(r, sh, height, seed=0x5EED, stats=False):
+    def frame(r, sh, height, seed=0x5EED, stats=False, batch_samples=None):
         st = r.render_into(sh.data_ptr(), row_begin=rank, row_end=height, row_stride=world,
-                           batch_samples=args.batch_samples, seed=seed, stats=stats)
+                           batch_samples=args.batch_samples if batch_samples is None else batch_samples, seed=seed,
+                           stats=stats)
         canvas = gather_canvas(sh, rank, world, height)
         return st, canvas
 
@@ -528,7 +535,8 @@ def main():
     total_rays = float(rays.item())
     proxy = None
     if world == 1 and not args.no_scaling_proxy:
-        proxy = {"headline": scaling_proxy(renderer, shard, H, 1e3 * t_max / args.steps)}
+        proxy = {"headline": scaling_proxy(renderer, shard, H, 1e3 * t_max / args.steps,
+                                           batch_samples=args.batch_samples)}
     renderer.close()
     del shard
 
@@ -543,7 +551,7 @@ def main():
         gstats = []
         for i in range(args.gi_steps):
             # a new seed per frame: the engine traces new photon maps (frt_frame_stats.photon_pass)
-            gst, _ = frame(gr, gshard, gscene.height, seed=0x61000 + i, stats=True)
+            gst, _ = frame(gr, gshard, gscene.height, seed=0x61000 + i, stats=True, batch_samples=args.gi_batch_samples)
             gstats.append(gst.as_dict())
         sync()
         g_elapsed = time.perf_counter() - g0
@@ -568,7 +576,8 @@ def main():
                       "jitter off) with the camera at 1920x1080x64; statistical parity (tests/test_gpu_stochastic.py)"}
         if world == 1 and not args.no_scaling_proxy and proxy is not None and args.gi_proxy:
             proxy["gi"] = scaling_proxy(gr, gshard, gscene.height, gi["ms_per_step"], reps=1,
-                                        seed_of=lambda n, r, i: 0x62000 + 16 * n + r)
+                                        seed_of=lambda n, r, i: 0x62000 + 16 * n + r,
+                                        batch_samples=args.gi_batch_samples)
         if gd.get("sub_launches", {}).get("k_gather_est"):
             gi["gather_est"] = {"ms_per_frame": round(gd["sub_ms"]["k_gather_est"], 3),
                                 "launches": gd["sub_launches"]["k_gather_est"],

@@ -2792,13 +2792,15 @@ static void launch_trace_redo_f(frt_scene_handle* h, const frt::Batch& B, const 
                        hits, h->err, h->tredo, (const unsigned*)(h->tredo + cap), cap);
 }
 
-// hn12: where the hits' refractive indices go (null: every index is one, or nobody reads them)
+// hn12: where the hits' refractive indices go (null: every index is one, or nobody reads them); jit: the path's
+// own rays (camera rays and their reflections: the scene-specialised closest hit where the scene has one; the
+// final gather's incoherent hemisphere rays measured faster on the generic walk, profiles/r04_ab_gi_trace.txt)
 static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
-                         frt::HitRec* hits = nullptr, int filter_casts = 0, double* hn12 = nullptr) {
+                         frt::HitRec* hits = nullptr, int filter_casts = 0, double* hn12 = nullptr, bool jit = false) {
     if (hits == nullptr) hits = h->hits;
     // the scene-specialised closest hit (frt_jit_trace), its undecided rays to the generic walk (k_trace_redo)
     static const bool jit_trace_env = !(std::getenv("FRT_JIT_TRACE") && std::atoi(std::getenv("FRT_JIT_TRACE")) == 0);
-    if (h->jit_trace && jit_trace_env && !filter_casts && hn12 == nullptr && n > 0 && n < ((int64_t)1 << 31)) {
+    if (jit && h->jit_trace && jit_trace_env && !filter_casts && hn12 == nullptr && n > 0 && n < ((int64_t)1 << 31)) {
         if (!grow(&h->tredo, h->tredo_cap, n + 2)) {  // (a list of every ray at worst, then its counter)
             unsigned cap = (unsigned)(h->tredo_cap - 2);
             unsigned* cnt = (unsigned*)(h->tredo + cap);
@@ -3949,7 +3951,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             const QueuedRay* q = d == 0 ? nullptr : L.q;
             {
                 KTimer t(h, st, d == 0 ? 5 : 0);
-                launch_trace(h, B, q, n, h->hits, 0, hn12);
+                launch_trace(h, B, q, n, h->hits, 0, hn12, true);
                 FRT_HIP(hipGetLastError());
             }
             {
