@@ -592,8 +592,9 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     // FRT_SHADE_ALG=0 builds: the vectors as the reference forms them (A/B runs).
                     constexpr bool kAlg = FRT_SHADE_ALG != 0;
                     const double ee = dot3(nr.eyev, nr.eyev);
-                    // pow_ns's exponent test once per node (the same Ns for every point)
+                    // pow_ns's exponent test once per node (the same Ns for every point: pow_plan / pow_apply)
                     const double nsd = nr.Ns;
+                    const PowPlan pplan = pow_plan(nsd);
                     // (the next point's load is issued before this point's arithmetic, so its latency hides
                     // behind the ~700 cycles of binary64 work instead of stalling every iteration)
                     auto points = [&](const double* pts) {
@@ -644,7 +645,7 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                                     ldh = dot3(lv, hv);
                                 }
                                 const double edh_inv = recip_shade(edh);
-                                double dist_term = kFactored ? pow_ns(ndh, nsd) * cdist
+                                double dist_term = kFactored ? pow_apply(ndh, nsd, pplan) * cdist
                                                              : (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
                                 double gc = 2.0 * ndh * edh_inv;
                                 double geo = fmin(1.0, fmin(gc * ned, gc * ndl));

@@ -332,6 +332,59 @@ __device__ __forceinline__ double pow_ns(double x, double y) {
     return pow_general(x, y);
 }
 
+// pow_ns's exponent analysis hoisted out of a loop whose exponent stays the same (the shading's light points:
+// the node's Ns). pow_plan runs where every lane of the loop is active; pow_apply(x, y, P) returns pow_ns(x, y)
+// bit for bit: the same products in the same order, by the one-exponent scalar loop when every lane of the wave
+// has the same integral exponent, else by the several-exponent loop (the squarings of the wave's largest
+// exponent: squarings past a lane's top bit leave its product alone), pow_general for the rest.
+struct PowPlan {
+    bool uniform;   // every lane: an integral exponent in [0, 4096), the same one (e0)
+    bool integral;  // this lane's exponent is integral and in range
+    unsigned e0;    // (uniform) the exponent
+    unsigned bits;  // (several) bit length of the wave's largest integral exponent
+};
+__device__ __forceinline__ PowPlan pow_plan(double y) {
+    PowPlan P;
+    P.integral = y >= 0.0 && y < 4096.0 && y == __builtin_floor(y);
+    const unsigned e = P.integral ? (unsigned)y : 0u;
+    P.e0 = (unsigned)__builtin_amdgcn_readfirstlane((int)e);
+    P.uniform = __ballot(!P.integral || e != P.e0) == 0ull;
+    P.bits = 0;
+    if (!P.uniform) {
+        unsigned emax = e;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) emax = max(emax, (unsigned)__shfl_xor((int)emax, o, 64));
+        P.bits = 32u - (unsigned)__clz((int)emax);
+    }
+    return P;
+}
+__device__ __forceinline__ double pow_apply(double x, double y, const PowPlan& P) {
+    double r = 1.0, b = x;
+    if (P.uniform) {
+        const unsigned e0 = P.e0;
+        bool first = true;
+        for (unsigned k = 0; (e0 >> k) != 0u; ++k) {
+            if ((e0 >> k) & 1u) {
+                r = first ? b : r * b;
+                first = false;
+            }
+            if ((e0 >> (k + 1)) == 0u) break;
+            b *= b;
+        }
+        return r;
+    }
+    if (P.integral) {
+        const unsigned e = (unsigned)y;
+#pragma nounroll
+        for (unsigned k = 0; k < P.bits; ++k) {
+            r = (e >> k) & 1u ? r * b : r;
+            b *= b;
+        }
+        return r;
+    }
+    return pow_general(x, y);
+}
+
 // ---- wave-aggregated counters ----
 // One atomic per wave instead of one per lane: a single shared counter taking
 // an atomic from every path node serialises at its L2 channel (the queue
