@@ -361,15 +361,19 @@ __device__ __forceinline__ PowPlan pow_plan(double y) {
 __device__ __forceinline__ double pow_apply(double x, double y, const PowPlan& P) {
     double r = 1.0, b = x;
     if (P.uniform) {
-        const unsigned e0 = P.e0;
-        bool first = true;
-        for (unsigned k = 0; (e0 >> k) != 0u; ++k) {
-            if ((e0 >> k) & 1u) {
-                r = first ? b : r * b;
-                first = false;
-            }
-            if ((e0 >> (k + 1)) == 0u) break;
-            b *= b;
+        // over the set bits (scalar control only: squarings up to the next set bit, then one product; no
+        // per-lane selects, which the bit-by-bit loop compiled to)
+        unsigned m = P.e0;
+        if (m == 0u) return 1.0;
+        unsigned pos = (unsigned)__builtin_ctz(m);
+        for (unsigned k = 0; k < pos; ++k) b *= b;
+        r = b;  // (the first product, 1 x b, is exact)
+        m &= m - 1u;
+        while (m != 0u) {
+            const unsigned k = (unsigned)__builtin_ctz(m);
+            for (; pos < k; ++pos) b *= b;
+            r *= b;
+            m &= m - 1u;
         }
         return r;
     }

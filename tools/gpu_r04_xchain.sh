@@ -3,8 +3,8 @@
 # (run via gpurun from the repo root)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_powplan.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_powbits.log 2>&1
 rc=$?
-tail -3 gpurun_out/pytest_powplan.log
+tail -3 gpurun_out/pytest_powbits.log
 [ $rc -ne 0 ] && exit $rc
-STEPS=3 TESTS= bash tools/gpu_ab_env.sh powplan "FRT_JIT_TRACE=1"
+STEPS=3 TESTS= bash tools/gpu_ab_env.sh powbits "FRT_JIT_TRACE=1"
