@@ -1511,7 +1511,7 @@ struct frt_scene_handle {
     int sub = 0;                       // sub-parts per part (frt_jit_sub_count) with jit_sub, else 0
     int sub_ps = 0;                    // samples per sub-part slot (frt_jit_sub_ps)
     const int32_t* light_psamp2 = nullptr;  // the sub-parts' samples (frt_jit_light_subparts), -1 padded
-    const float* light_sbox = nullptr;      // the sub-parts' boxes (single-row lights), binary32 outward
+    const float* light_sbox = nullptr;      // the sub-parts' boxes over every cache row, binary32 outward
     uint32_t* slist = nullptr;         // the tile sub-pairs left mixed (frt_jit_sub's list), kMixSegs segments
     int64_t slist_cap = 0;
     uint64_t sub_pairs = 0, sub_mixed = 0;
@@ -1520,6 +1520,11 @@ struct frt_scene_handle {
     int32_t* tredo = nullptr;          // rays frt_jit_trace hands to the generic walk (k_trace_redo), + counter
     int64_t tredo_cap = 0;
     int subtile = 0;                   // path nodes per sub-tile (frt_jit_subtile_size) with jit_subtile, else 0
+    // the (node, sample) pairs the sub-part / sub-tile stages leave: decided by frt_jit_beam_list one node beam per
+    // lane (FRT_JIT_NODE_BEAM=1), or walked by frt_jit_shadow directly (the default: a node's beam to one sample is
+    // one ray, and the per-ray walk costs a third of the beam walk's instructions; round 5, profiles/r05_ab_nodebeam.txt:
+    // headline 41.5 -> 36.4 ms, shipped light 90.5 -> 76.4 ms)
+    bool node_beam = false;
     float* stbox = nullptr;            // the level's sub-tile boxes (k_prepare): 6 floats per sub-tile
     int64_t stbox_cap = 0;
     uint32_t* s2list = nullptr;        // the sub-tile pairs left mixed (frt_jit_subtile's list)
@@ -2378,6 +2383,15 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             // (the closest-hit kernel writes n1 = n2 = 1: scenes with refractive indices other than one keep k_trace)
             h->jit_trace = sc->config.all_ni_one ? fns.trace : nullptr;
             h->subtile = fns.subtile ? frt_jit_subtile_size() : 0;
+            {
+                // multi-row lights (the shipped area-light cache): the sub-tile stage decides few of the (tile, sample)
+                // pairs the sub-part stage leaves — the sample's point lies anywhere in its light cell for the sub-tile's
+                // nodes — so it runs only when FRT_JIT_SUBTILE asks for it (round 5, profiles/r05_ab_nodebeam.txt: it
+                // cut the shipped frame's per-ray lanes by 11 % for 6.5 ms; without it 76.4 -> 72.1 ms)
+                bool multi = false;
+                for (int l = 0; l < sc->num_lights; ++l) multi = multi || sc->lights[l].rows > 1;
+                if (multi && !std::getenv("FRT_JIT_SUBTILE")) h->subtile = 0;
+            }
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
                 void* p = nullptr;
@@ -2391,76 +2405,87 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                 const char* beam_env = std::getenv("FRT_JIT_BEAM");
                 h->jit_beam_on = !(beam_env && std::strcmp(beam_env, "0") == 0);
                 // each light's parts (frt_jit_light_parts) and, per cache row, the box of each part's points,
-                // rounded outward to binary32
+                // rounded outward to binary32; with a multi-row light (the shipped area-light cache) also, after
+                // every light's row boxes, each part's box over all rows (the tile kernel's: a tile's nodes draw
+                // different rows). The reference's CMJ keeps sample (u, v) of every row in light cell (u, v)
+                // (sampler.c:423-460: the x shuffle swaps within a column, the y shuffle within a row), so the
+                // union stays the size of the part's cells.
                 std::vector<float> box;
                 std::vector<int32_t> psamp;
                 const int PS = frt_jit_part_size();
-                for (int l = 0; l < sc->num_lights; ++l) {
-                    const frt_light& lt = sc->lights[l];
-                    std::vector<int32_t> order;
-                    const int np = frt_jit_light_parts(lt, sc->light_points, PS, order);
-                    psamp.insert(psamp.end(), order.begin(), order.end());
-                    for (int r = 0; r < std::max(1, lt.rows); ++r) {
-                        for (int p = 0; p < np; ++p) {
-                            double pl[3] = {INFINITY, INFINITY, INFINITY}, ph[3] = {-INFINITY, -INFINITY, -INFINITY};
-                            for (int k = 0; k < PS; ++k) {
-                                const int q = order[(size_t)p * PS + k];
-                                if (q < 0) continue;
-                                const double* pt = sc->light_points + lt.points + 3 * ((int64_t)r * lt.num_samples + q);
-                                for (int a = 0; a < 3; ++a) {
-                                    pl[a] = std::min(pl[a], pt[a]);
-                                    ph[a] = std::max(ph[a], pt[a]);
-                                }
-                            }
+                auto push_box = [](std::vector<float>& v, const double* pl, const double* ph) {
+                    for (int a = 0; a < 3; ++a) {
+                        float f = (float)pl[a];
+                        if ((double)f > pl[a]) f = std::nextafter(f, -INFINITY);
+                        v.push_back(f);
+                    }
+                    for (int a = 0; a < 3; ++a) {
+                        float f = (float)ph[a];
+                        if ((double)f < ph[a]) f = std::nextafter(f, INFINITY);
+                        v.push_back(f);
+                    }
+                };
+                // the box of samples idx[0..cnt) (-1 entries skipped) over rows [r0, r1)
+                auto sample_box = [&](const frt_light& lt, const int32_t* idx, int cnt, int r0, int r1, double* pl, double* ph) {
+                    for (int a = 0; a < 3; ++a) {
+                        pl[a] = INFINITY;
+                        ph[a] = -INFINITY;
+                    }
+                    for (int r = r0; r < r1; ++r)
+                        for (int k = 0; k < cnt; ++k) {
+                            const int q = idx[k];
+                            if (q < 0) continue;
+                            const double* pt = sc->light_points + lt.points + 3 * ((int64_t)r * lt.num_samples + q);
                             for (int a = 0; a < 3; ++a) {
-                                float f = (float)pl[a];
-                                if ((double)f > pl[a]) f = std::nextafter(f, -INFINITY);
-                                box.push_back(f);
-                            }
-                            for (int a = 0; a < 3; ++a) {
-                                float f = (float)ph[a];
-                                if ((double)f < ph[a]) f = std::nextafter(f, INFINITY);
-                                box.push_back(f);
+                                pl[a] = std::min(pl[a], pt[a]);
+                                ph[a] = std::max(ph[a], pt[a]);
                             }
                         }
+                };
+                bool multi_row = false;
+                std::vector<std::vector<int32_t>> orders((size_t)sc->num_lights);
+                for (int l = 0; l < sc->num_lights; ++l) {
+                    const frt_light& lt = sc->lights[l];
+                    multi_row = multi_row || lt.rows > 1;
+                    std::vector<int32_t>& order = orders[(size_t)l];
+                    const int np = frt_jit_light_parts(lt, sc->light_points, PS, order);
+                    psamp.insert(psamp.end(), order.begin(), order.end());
+                    for (int r = 0; r < std::max(1, lt.rows); ++r)
+                        for (int p = 0; p < np; ++p) {
+                            double pl[3], ph[3];
+                            sample_box(lt, order.data() + (size_t)p * PS, PS, r, r + 1, pl, ph);
+                            push_box(box, pl, ph);
+                        }
+                }
+                for (int l = 0; multi_row && l < sc->num_lights; ++l) {
+                    const frt_light& lt = sc->lights[l];
+                    const int np = (int)(orders[(size_t)l].size() / (size_t)PS);
+                    for (int p = 0; p < np; ++p) {
+                        double pl[3], ph[3];
+                        sample_box(lt, orders[(size_t)l].data() + (size_t)p * PS, PS, 0, std::max(1, lt.rows), pl, ph);
+                        push_box(box, pl, ph);
                     }
                 }
                 h->light_psamp = upload(h, psamp.data(), psamp.size(), rc);
                 h->light_aabb = upload(h, box.data(), box.size(), rc);
-                if (h->sub > 0) {  // the sub-parts (single-row lights): samples and boxes by (global part, sub-part)
+                {
+                    const char* nb = std::getenv("FRT_JIT_NODE_BEAM");
+                    h->node_beam = nb && std::atoi(nb) != 0;
+                }
+                if (h->sub > 0) {  // the sub-parts: samples and boxes (over every cache row) by (global part, sub-part)
                     std::vector<int32_t> ps2;
                     std::vector<float> sbox;
                     const int Q = h->sub;
-                    size_t off = 0;
                     for (int l = 0; l < sc->num_lights; ++l) {
                         const frt_light& lt = sc->lights[l];
                         const int np = std::max(1, (lt.num_samples + PS - 1) / PS);
-                        std::vector<int32_t> order(psamp.begin() + (ptrdiff_t)off, psamp.begin() + (ptrdiff_t)(off + (size_t)np * PS));
-                        off += (size_t)np * PS;
                         std::vector<int32_t> order2;
-                        h->sub_ps = frt_jit_light_subparts(lt, sc->light_points, order, PS, Q, order2);
+                        h->sub_ps = frt_jit_light_subparts(lt, sc->light_points, orders[(size_t)l], PS, Q, order2);
                         ps2.insert(ps2.end(), order2.begin(), order2.end());
                         for (int p = 0; p < np * Q; ++p) {
-                            double pl[3] = {INFINITY, INFINITY, INFINITY}, ph[3] = {-INFINITY, -INFINITY, -INFINITY};
-                            for (int k = 0; k < h->sub_ps; ++k) {
-                                const int q = order2[(size_t)p * h->sub_ps + k];
-                                if (q < 0) continue;
-                                const double* pt = sc->light_points + lt.points + 3 * (int64_t)q;
-                                for (int a = 0; a < 3; ++a) {
-                                    pl[a] = std::min(pl[a], pt[a]);
-                                    ph[a] = std::max(ph[a], pt[a]);
-                                }
-                            }
-                            for (int a = 0; a < 3; ++a) {
-                                float f = (float)pl[a];
-                                if ((double)f > pl[a]) f = std::nextafter(f, -INFINITY);
-                                sbox.push_back(f);
-                            }
-                            for (int a = 0; a < 3; ++a) {
-                                float f = (float)ph[a];
-                                if ((double)f < ph[a]) f = std::nextafter(f, INFINITY);
-                                sbox.push_back(f);
-                            }
+                            double pl[3], ph[3];
+                            sample_box(lt, order2.data() + (size_t)p * h->sub_ps, h->sub_ps, 0, std::max(1, lt.rows), pl, ph);
+                            push_box(sbox, pl, ph);
                         }
                     }
                     h->light_psamp2 = upload(h, ps2.data(), ps2.size(), rc);
@@ -2906,6 +2931,8 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         uint32_t nn = (uint32_t)n;
         uint32_t segcap = 0;
         uint64_t total_mixed = 0;
+        const uint32_t* direct_in = nullptr;  // (the sub / sub-tile list walked by the per-ray kernel directly)
+        uint32_t direct_subq = 0, direct_nodes = 0;
         if (h->jit_beam_on) {
             frt::jit::SegTable tseg{};
             uint32_t tsegcap = 0;
@@ -2932,7 +2959,8 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 const uint32_t* no_list = nullptr;
                 uint32_t zero = 0;
                 void* targs[] = {&h->S, (void*)&B, (void*)&rec, &ntp, &nn, (void*)&tb, (void*)&no_list, &tseg, &zero, &zero,
-                                 &h->light_aabb, &counts, &h->tlist, &h->mcount, &tsegcap, &h->err, &h->jit_stats};
+                                 &h->light_aabb, &counts, &h->tlist, &h->mcount, &tsegcap, &h->err, &h->jit_stats,
+                                 &h->light_psamp2};
                 hipError_t le;
                 {
                     KTimer tt(h, h->cur_st, 12);
@@ -2980,7 +3008,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                             uint32_t b0u = (uint32_t)b0;
                             void* sargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&tb, &h->tlist, (void*)&sseg, &b0u,
                                              &tsegcap, &h->light_sbox, &counts, &h->slist, &h->mcount, (void*)&ssegcap, &h->err,
-                                             &h->jit_stats};
+                                             &h->jit_stats, &h->light_psamp2};
                             se = hipModuleLaunchKernel((hipFunction_t)h->jit_sub, (unsigned)std::min(max_blocks, sblocks - b0), 1, 1,
                                                        frt::kTraceBlock, 1, 1, 0, h->stream, sargs, nullptr);
                         }
@@ -3035,7 +3063,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                                 uint32_t b0u = (uint32_t)b0;
                                 void* uargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&stb, &h->slist, (void*)&s1seg,
                                                  &b0u, (void*)&ssegcap, &h->light_sbox, &counts, &h->s2list, &h->mcount,
-                                                 (void*)&s2segcap, &h->err, &h->jit_stats};
+                                                 (void*)&s2segcap, &h->err, &h->jit_stats, &h->light_psamp2};
                                 ue = hipModuleLaunchKernel((hipFunction_t)h->jit_subtile, (unsigned)std::min(max_blocks, tblocks - b0),
                                                            1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, uargs, nullptr);
                             }
@@ -3070,6 +3098,17 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     listed = 0;
                 }
             }
+            if (subbed && !h->node_beam && list_in != h->tlist) {
+                // the sub-part (sub-tile) stage's list goes to the per-ray kernel as it is (host_mcount holds its
+                // counts): each entry's nodes times its sub-part's samples, one lane per (node, sample)
+                direct_in = list_in;
+                direct_subq = list_in == h->s2list ? 3u : 2u;
+                direct_nodes = (uint32_t)(list_in == h->s2list ? h->subtile : h->tile);
+                segcap = list_segcap;
+                for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
+                h->node_pairs += total_mixed * direct_nodes;
+                h->node_mixed += total_mixed * direct_nodes;
+            } else {
             // the mixed list of the node pairs (the per-ray kernel's): per segment, every lane of the blocks that
             // append to it
             const int64_t pblocks = tiled ? (int64_t)list_blocks : (npairs + frt::kTraceBlock - 1) / frt::kTraceBlock;
@@ -3096,7 +3135,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         uint32_t b0u = (uint32_t)b0;
                         void* largs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&no_box, (void*)&list_in, &tseg, &b0u,
                                          &list_segcap, (void*)&list_boxes, &counts, nout, &h->mcount, &segcap, &h->err,
-                                         &h->jit_stats};
+                                         &h->jit_stats, &h->light_psamp2};
                         le = hipModuleLaunchKernel((hipFunction_t)h->jit_list, (unsigned)std::min(max_blocks, list_blocks - b0), 1, 1,
                                                    frt::kTraceBlock, 1, 1, 0, h->stream, largs, nullptr);
                     }
@@ -3108,7 +3147,8 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     frt::jit::SegTable no_seg{};
                     uint32_t zero = 0;
                     void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &nn, (void*)&no_box, (void*)&no_list, &no_seg, &zero, &zero,
-                                     &h->light_aabb, &counts, nout, &h->mcount, &segcap, &h->err, &h->jit_stats};
+                                     &h->light_aabb, &counts, nout, &h->mcount, &segcap, &h->err, &h->jit_stats,
+                                     &h->light_psamp2};
                     le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1, 1,
                                                frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
                     h->node_pairs += (uint64_t)npairs;
@@ -3129,6 +3169,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 return;
             for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
             h->node_mixed += total_mixed;
+            }
         } else {
             segcap = (uint32_t)std::max<int64_t>(1, npairs);
             if (grow(&h->mixed, h->mixed_cap, 2 * (int64_t)segcap * kMixSegs)) {  // (out of memory): the generic walk
@@ -3142,8 +3183,9 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         uint32_t all_pairs = h->jit_beam_on ? 0u : 1u;
         // lanes per pair (a part of frt_jit_part_size() samples, or a sub-part's slot after frt_jit_sub);
         // tid / lpp by multiply-shift
-        uint32_t subq = subbed ? 1u : 0u;
-        uint32_t lpp = subbed ? (uint32_t)h->sub_ps : (uint32_t)frt_jit_part_size();
+        uint32_t subq = direct_in ? direct_subq : subbed ? 1u : 0u;
+        uint32_t lpp = direct_in ? direct_nodes * (uint32_t)h->sub_ps : subbed ? (uint32_t)h->sub_ps : (uint32_t)frt_jit_part_size();
+        const uint32_t* mixed_in = direct_in ? direct_in : h->mixed;
         uint32_t shift = 32;
         while ((1u << (shift - 32)) < lpp) ++shift;  // 32 + ceil(log2 lpp)
         const uint64_t magic = (uint64_t)((((unsigned __int128)1 << shift) + lpp - 1) / lpp);
@@ -3177,9 +3219,9 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 b0 = (uint32_t)(li * max_blocks);
                 grid = std::min<uint64_t>(max_blocks, nblk - b0);
             }
-            void* args[] = {&h->S, (void*)&B, (void*)&rec, &total, &m0, &h->mixed, &seg, &b0, &segcap, &all_pairs,
+            void* args[] = {&h->S, (void*)&B, (void*)&rec, &total, &m0, (void*)&mixed_in, &seg, &b0, &segcap, &all_pairs,
                             &h->light_psamp, &subq, &h->light_psamp2, &lpp, (void*)&magic,
-                            &shift, &spn, &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats};
+                            &shift, &spn, &counts, &h->redo, &h->redo_count, &h->redo_cap, &h->err, &h->jit_stats, &nn};
             const hipError_t le = hipModuleLaunchKernel((hipFunction_t)h->jit_shadow, (unsigned)grid,
                                                         1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, args, nullptr);
             if (le != hipSuccess) {
@@ -3957,7 +3999,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             }
             {
                 KTimer t(h, st, 6);
-                // tile boxes for frt_jit_tile (scene-specialised shadow kernels with single-row lights)
+                // tile boxes for frt_jit_tile (scene-specialised shadow kernels)
                 const bool tiles = h->tile > 0 && h->jit_shadow && h->jit_beam_on && h->S.cfg.include_direct &&
                                    h->samples_per_node > 0;
                 int tl = 0;

@@ -120,6 +120,12 @@ SCENES = {
     # BASELINE configs[4]: the shipped GI configuration (1M photons, 8x8 final gather) at 1920x1080x64
     "cornell_gi_1920x1080_8x8": ("scenes/cornell_box/cornell_box.yml",
                                  {"size": (1920, 1080), "steps": (8, 8), "no_golden": True}),
+    # ---- round 5 ----
+    # the direct-lighting frame as shipped (65535-row jittered light cache, camera jitter off as in
+    # cornell_box.yml) at the headline size, GI off: bench.py's "shipped" line; parity by row bands through
+    # every shadow stage vs the generic walk at a fixed seed (tests/test_jit.py) and by cornell_shipped_48_4x4
+    "cornell_shipped_1920x1080_8x8": ("scenes/cornell_box/cornell_box.yml",
+                                      {"size": (1920, 1080), "steps": (8, 8), "gi_off": True, "no_golden": True}),
     # GI statistical goldens at 64x64 (round 2: more power than the 24 / 32 px ones)
     "cornell_gi_64": ("scenes/cornell_box/cornell_box.yml",
                       {"size": (64, 64), "threads": 8, "extra_seeds": STOCHASTIC_SEEDS, "gi": {}}),

@@ -119,19 +119,19 @@ sys.path.insert(0, {tests!r})
 from conftest import load_scene
 from fast_ray_tracer_amd.runtime import GpuRenderer
 r = GpuRenderer(load_scene({name!r}))
-img, st = r.render(stats=True)
+img, st = r.render(stats=True, **{kw!r})
 d = st.as_dict()
 np.save({out!r}, img)
 print("STATS", d["shadow_jit"], d["shadow_tile_pairs"], d["shadow_sub_pairs"])
 """
 
 
-def _render_env_process(name, env, out):
+def _render_env_process(name, env, out, **kw):
     """Render in a fresh process (the tile size and sub-part count are read once per process)."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    p = subprocess.run([sys.executable, "-c", _ENV_RENDER.format(tests=here, name=name, out=str(out))],
+    p = subprocess.run([sys.executable, "-c", _ENV_RENDER.format(tests=here, name=name, out=str(out), kw=kw)],
                        env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     stats = [ln.split()[1:] for ln in p.stdout.splitlines() if ln.startswith("STATS")][-1]
@@ -139,7 +139,8 @@ def _render_env_process(name, env, out):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "reflect_refract_test_150", "test_scene_120"])
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "reflect_refract_test_150", "test_scene_120",
+                                  "cornell_shipped_48_4x4"])
 def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
     """The tile pair kernel (frt_jit_tile: runs of consecutive path nodes from their origin box), the sub-part pass
     after it (frt_jit_sub: the tile pairs left mixed, their parts split into sub-parts; 16 single samples of the
@@ -152,7 +153,10 @@ def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
     for i, env in enumerate(({"FRT_JIT_TILE": "2"}, {"FRT_JIT_TILE": "32", "FRT_JIT_SUB": "0"},
                              {"FRT_JIT_TILE": "32", "FRT_JIT_ORDER": "0", "FRT_JIT_PART": "17", "FRT_JIT_SUB": "4"},
                              {"FRT_JIT_TILE": "64", "FRT_JIT_ORDER": "2"},
-                             {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"})):
+                             {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"},
+                             # the sub-tile (sub-part) stage's list walked ray by ray without the node pair kernel
+                             {"FRT_JIT_NODE_BEAM": "0"}, {"FRT_JIT_NODE_BEAM": "0", "FRT_JIT_SUBTILE": "0"},
+                             {"FRT_JIT_NODE_BEAM": "1"})):
         img, st = _render_env_process(name, env, tmp_path / ("j%d.npy" % i))
         assert st[0] == 1 and st[1] > 0, (env, st)
         if env.get("FRT_JIT_SUB") != "0":
@@ -172,3 +176,25 @@ def test_jit_closest_hit_equals_generic_walk(built, name, tmp_path):
     ref, _ = _render_env_process(name, {"FRT_JIT_TRACE": "0"}, tmp_path / "g.npy")
     img, _ = _render_env_process(name, {}, tmp_path / "j.npy")
     assert np.array_equal(img, ref), name
+
+
+@pytest.mark.gpu
+def test_tile_kernels_on_shipped_multi_row_light(built, tmp_path):
+    """The reference's shipped light (cornell_box.yml: 65 535 jittered cache rows, each path node drawing its own row):
+    the tile, sub-part and sub-tile stages decide beams against part boxes that hold for every row (CMJ keeps sample
+    (u, v) of every row in light cell (u, v)), frt_jit_beam_list against the node's own row. At a fixed seed, row bands
+    of the shipped 1920x1080x64 frame through the whole hierarchy, through the node pair kernel alone
+    (FRT_JIT_TILE=0) and through the generic walk are bit-identical, and the tile stages ran — with the sub-tile stage's
+    list walked ray by ray (the default for multi-row lights), through frt_jit_beam_list (FRT_JIT_NODE_BEAM=1) and
+    without the sub-tile stage."""
+    for rows in ((300, 306), (700, 706)):
+        kw = {"row_begin": rows[0], "row_end": rows[1], "seed": 0x5EED}
+        ref, st = _render_env_process("cornell_shipped_1920x1080_8x8", {"FRT_JIT": "0"}, tmp_path / "g.npy", **kw)
+        assert st[0] == 0
+        for i, env in enumerate(({}, {"FRT_JIT_NODE_BEAM": "1"}, {"FRT_JIT_SUBTILE": "0"})):
+            img, st = _render_env_process("cornell_shipped_1920x1080_8x8", env, tmp_path / ("t%d.npy" % i), **kw)
+            assert st[0] == 1 and st[1] > 0 and st[2] > 0, (env, st)
+            assert np.array_equal(img, ref), (rows, env)
+        img0, st0 = _render_env_process("cornell_shipped_1920x1080_8x8", {"FRT_JIT_TILE": "0"}, tmp_path / "n.npy", **kw)
+        assert st0[0] == 1 and st0[1] == 0, st0
+        assert np.array_equal(img0, ref), rows
