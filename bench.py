@@ -612,6 +612,7 @@ def main():
             # rays walked one by one (primary + secondary + the shadow rays of the pairs the pair kernels could
             # not decide): `value` counts every shadow ray, also those decided for a whole beam at once
             "rays_per_frame_walked": walked_rays,
+            "lit_nodes_per_frame": d.get("lit_nodes"),
             "walked_mrays_s": round(walked_rays * world * args.steps / t_max / 1e6, 3),
             "reference_equivalent_rays_per_frame": ref_rays,
             "reference_equivalent_mrays_s": round(ref_rays * args.steps / t_max / 1e6, 3) if ref_rays else None,

@@ -23,6 +23,7 @@
 // (refraction through opaque surfaces, Tf = 0: 94-100 % of the reference's
 // secondary rays) are not traced; their contribution is an exact 0.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <array>
@@ -552,10 +553,25 @@ __global__ void __launch_bounds__(kTraceBlock) k_shadow_redo(DevScene S, Batch B
 #ifndef FRT_SHADE_ALG
 #define FRT_SHADE_ALG 1
 #endif
+#ifndef FRT_SHADE_SKIP
+#define FRT_SHADE_SKIP 1
+#endif
+// FRT_SHADE_FMA (default 1): the light point's three dot products (|v|^2, v.n, v.e) as one product and two fused
+// multiply-adds instead of three products and two sums (each within an ulp of the separately rounded sum, like the
+// Newton-refined estimates beside them); 0: the reference's separately rounded operations (A/B builds)
+#ifndef FRT_SHADE_FMA
+#define FRT_SHADE_FMA 1
+#endif
+__device__ __forceinline__ double dot3_shade(const double* a, const double* b) {
+    if (FRT_SHADE_FMA) return __builtin_fma(a[0], b[0], __builtin_fma(a[1], b[1], a[2] * b[2]));
+    return dot3(a, b);
+}
 // lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725): the
 // A, D, S triples of path node i into out (out[4k + c]: term k, channel c)
+// (lds_row: k_shade_lit's per-wave LDS staging of a multi-row light's row, kLdsPoints points; nullptr elsewhere)
+constexpr int kLdsPoints = 128;
 __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, const NodeRec& nr, int64_t i,
-                                           const int32_t* __restrict__ counts, double* out) {
+                                           const int32_t* __restrict__ counts, double* out, double* lds_row = nullptr) {
     double sA[3] = {0, 0, 0}, sD[3] = {0, 0, 0}, sS[3] = {0, 0, 0};
     if (S.cfg.include_direct) {
         for (int li = 0; li < S.num_lights; ++li) {
@@ -595,83 +611,154 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     // pow_ns's exponent test once per node (the same Ns for every point: pow_plan / pow_apply)
                     const double nsd = nr.Ns;
                     const PowPlan pplan = pow_plan(nsd);
-                    // (the next point's load is issued before this point's arithmetic, so its latency hides
-                    // behind the ~700 cycles of binary64 work instead of stalling every iteration)
-                    auto points = [&](const double* pts) {
-                        const int ns = L.num_samples;
-                        double nx[3] = {pts[0], pts[1], pts[2]};
-                        for (int p = 0; p < ns; ++p) {
-                            const double lp[3] = {nx[0], nx[1], nx[2]};
-                            const double* q = pts + 3 * min(p + 1, ns - 1);
-                            nx[0] = q[0];
-                            nx[1] = q[1];
-                            nx[2] = q[2];
-                            double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
-                            double lv[3] = {0.0, 0.0, 0.0}, ldn, m2 = 0.0, rl = 0.0;
-                            if (kAlg) {
-                                m2 = dot3(diff, diff);
-                                rl = rsqrt_shade(m2);
-                                ldn = dot3(diff, nr.normalv) * rl;
+                    // The specular tail (FRT_SHADE_SKIP, default 1): with Ns = 200 the lobe (n.h)^Ns is below 2^-60 of
+                    // the point's diffuse term for most (node, point) pairs, yet every lane paid the reciprocal, the
+                    // power and the quotient. A point's specular terms are at most (|Ks| + |1 - Ks|) I brdf per channel
+                    // (F <= 1: 0 <= 1 - l.h <= 1), brdf <= cdist (n.h)^Ns / (4 (l.n) (n.e)) (G <= 1), and its diffuse
+                    // term is Kd I (l.n); when cdist (n.h)^Ns < 2^-62 rK (l.n)^2 (n.e), rK = min_k Kd_k / (|Ks_k| +
+                    // |1 - Ks_k|), the point's specular terms lie below 2^-62 of its diffuse ones and are left out
+                    // (the node's colour moves by less than 2^-60 of itself; the Newton-refined estimates above are
+                    // within 2^-46). Tested in binary32 logarithms with 4 binades of margin (the conversions and
+                    // v_log_f32 are within 1e-4 of a binade at Ns <= 4096). Per lane: a lane's result does not
+                    // depend on its wave; the arithmetic is skipped where every lane of the wave skips.
+                    float skip_c = __builtin_huge_valf();  // log2(cdist / (rK (n.e))) + 62 + 4; +inf: never skip
+                    if (FRT_SHADE_SKIP && kFactored && kAlg && S.cfg.include_diffuse && S.cfg.include_spec_highlight &&
+                        nsd >= 2.0 && nsd <= 4096.0 && ned > 0x1p-100) {
+                        double rk = 1.0;
+                        for (int k = 0; k < 3; ++k) rk = fmin(rk, nr.Kd[k] / (fabs(nr.Ks[k]) + fabs(1.0 - nr.Ks[k])));
+                        if (rk > 0x1p-100) skip_c = __log2f((float)(cdist / (rk * ned))) + 66.0f;
+                    }
+                    const float nsf = (float)nsd;
+                    // one light point's terms (lp: the point)
+                    auto term = [&](const double* lp) {
+                        double diff[3] = {lp[0] - nr.over_point[0], lp[1] - nr.over_point[1], lp[2] - nr.over_point[2]};
+                        double lv[3] = {0.0, 0.0, 0.0}, ldn, m2 = 0.0, rl = 0.0;
+                        if (kAlg) {
+                            m2 = dot3_shade(diff, diff);
+                            rl = rsqrt_shade(m2);
+                            ldn = dot3_shade(diff, nr.normalv) * rl;
+                        } else {
+                            normalize3_shade(diff, lv);
+                            ldn = dot3(lv, nr.normalv);
+                        }
+                        if (S.cfg.include_diffuse && ldn >= 0.0) {
+                            if (kFactored) {
+                                sum_ldn += ldn;
                             } else {
-                                normalize3_shade(diff, lv);
-                                ldn = dot3(lv, nr.normalv);
-                            }
-                            if (S.cfg.include_diffuse && ldn >= 0.0) {
-                                if (kFactored) {
-                                    sum_ldn += ldn;
-                                } else {
-                                    for (int k = 0; k < 3; ++k) {
-                                        double cc = nr.Kd[k] * L.intensity[k];
-                                        cc *= ldn;
-                                        dacc[k] += cc;
-                                    }
+                                for (int k = 0; k < 3; ++k) {
+                                    double cc = nr.Kd[k] * L.intensity[k];
+                                    cc *= ldn;
+                                    dacc[k] += cc;
                                 }
                             }
-                            if (S.cfg.include_spec_highlight && ldn >= 0.0) {
-                                double ndl, ndh, edh, ldh;
-                                if (kAlg) {
-                                    ndl = ldn;
-                                    const double el = dot3(diff, nr.eyev) * rl, ll = (m2 * rl) * rl;
-                                    const double rh = rsqrt_shade(ll + 2.0 * el + ee);
-                                    ndh = fmax(0.0, (ldn + ned) * rh);
-                                    edh = fmax(0.0, (el + ee) * rh);
-                                    ldh = (ll + el) * rh;
-                                } else {
-                                    ndl = dot3(nr.normalv, lv);
-                                    double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
-                                    normalize3_shade(tmp, hv);
-                                    ndh = fmax(0.0, dot3(nr.normalv, hv));
-                                    edh = fmax(0.0, dot3(nr.eyev, hv));
-                                    ldh = dot3(lv, hv);
-                                }
-                                const double edh_inv = recip_shade(edh);
-                                double dist_term = kFactored ? pow_apply(ndh, nsd, pplan) * cdist
-                                                             : (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
-                                double gc = 2.0 * ndh * edh_inv;
-                                double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
-                                // pow(1 - ldh, 5.0) (renderer.c:969) by squaring: within an ulp or two of the
-                                // reference's libm pow, like the device pow it replaces
-                                const double om = 1.0 - ldh, om2 = om * om;
-                                double factor = om2 * om2 * om;
-                                double brdf = div_shade(dist_term * geo, 4.0 * ndl * ned);
-                                if (kFactored) {
-                                    sum_b += brdf;
-                                    sum_fb += factor * brdf;
-                                } else {
-                                    for (int k = 0; k < 3; ++k) {
-                                        double f = nr.Ks[k] + (1.0 - nr.Ks[k]) * factor;
-                                        sacc[k] += f * L.intensity[k] * brdf;
-                                    }
+                        }
+                        if (S.cfg.include_spec_highlight && ldn >= 0.0) {
+                            double ndl, ndh, edh, ldh;
+                            if (kAlg) {
+                                ndl = ldn;
+                                const double el = dot3_shade(diff, nr.eyev) * rl, ll = (m2 * rl) * rl;
+                                const double rh = rsqrt_shade(ll + 2.0 * el + ee);
+                                ndh = fmax(0.0, (ldn + ned) * rh);
+                                edh = fmax(0.0, (el + ee) * rh);
+                                ldh = (ll + el) * rh;
+                                // (the specular tail test; NaN compares false: not skipped)
+                                const bool tail = ldn > 0x1p-100 &&
+                                                  nsf * __log2f((float)ndh) - 2.0f * __log2f((float)ldn) + skip_c < 0.0f;
+                                if (__ballot(!tail) == 0ull) return;
+                                if (tail) return;
+                            } else {
+                                ndl = dot3(nr.normalv, lv);
+                                double tmp[3] = {lv[0] + nr.eyev[0], lv[1] + nr.eyev[1], lv[2] + nr.eyev[2]}, hv[3];
+                                normalize3_shade(tmp, hv);
+                                ndh = fmax(0.0, dot3(nr.normalv, hv));
+                                edh = fmax(0.0, dot3(nr.eyev, hv));
+                                ldh = dot3(lv, hv);
+                            }
+                            const double edh_inv = recip_shade(edh);
+                            double dist_term = kFactored ? pow_apply(ndh, nsd, pplan) * cdist
+                                                         : (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
+                            double gc = 2.0 * ndh * edh_inv;
+                            double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
+                            // pow(1 - ldh, 5.0) (renderer.c:969) by squaring: within an ulp or two of the
+                            // reference's libm pow, like the device pow it replaces
+                            const double om = 1.0 - ldh, om2 = om * om;
+                            double factor = om2 * om2 * om;
+                            double brdf = div_shade(dist_term * geo, 4.0 * ndl * ned);
+                            if (kFactored) {
+                                sum_b += brdf;
+                                sum_fb += factor * brdf;
+                            } else {
+                                for (int k = 0; k < 3; ++k) {
+                                    double f = nr.Ks[k] + (1.0 - nr.Ks[k]) * factor;
+                                    sacc[k] += f * L.intensity[k] * brdf;
                                 }
                             }
                         }
                     };
                     const double* row0 = S.light_points + L.points;
+                    const int ns = L.num_samples;
+                    // a wave-uniform row: the same point in every lane, so its address is wave-uniform and the loads go
+                    // through the scalar cache (the point's coordinates in SGPRs, no vector memory latency)
+                    auto uniform_points = [&](const double* up) {
+                        const double* sp = (const double*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                                (int)(uint32_t)(uint64_t)up)) |
+                                                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                                 (int)(uint32_t)((uint64_t)up >> 32))
+                                                             << 32));
+                        double a[3] = {sp[0], sp[1], sp[2]};
+                        for (int p = 0; p < ns; ++p) {  // (the next point's scalar loads ahead of this one's arithmetic)
+                            const double lp[3] = {a[0], a[1], a[2]};
+                            const double* q = sp + 3 * min(p + 1, ns - 1);
+                            a[0] = q[0];
+                            a[1] = q[1];
+                            a[2] = q[2];
+                            term(lp);
+                        }
+                    };
+                    const int row = L.rows <= 1 ? 0 : light_row(L, B.seed, nr.key, li, 1);
+                    const int ra = __builtin_amdgcn_readfirstlane(row);
                     if (L.rows <= 1) {
-                        points(row0);  // one cache row: the same points in every lane, through the scalar cache
+                        uniform_points(row0);  // one cache row
+                    } else if (__ballot(row != ra) == 0ull && lds_row != nullptr) {
+                        // the wave shares its row (the lit list in row order): the row into the wave's LDS in one
+                        // coalesced round trip by the active lanes, then every lane reads the same point (a broadcast).
+                        // Through the scalar cache instead, every point was a trip to L2: the waves of a CU read
+                        // different rows, more than the scalar cache holds.
+                        const double* rp = row0 + 3 * (int64_t)ra * ns;
+                        const unsigned long long act = __ballot(true);
+                        const int lane = (int)(threadIdx.x & 63);
+                        const int rank = __popcll(act & ((1ull << lane) - 1)), nact = __popcll(act);
+                        for (int c0 = 0; c0 < ns; c0 += kLdsPoints) {
+                            const int cn = min(kLdsPoints, ns - c0);
+                            __builtin_amdgcn_wave_barrier();
+                            for (int w = rank; w < 3 * cn; w += nact) lds_row[w] = rp[3 * c0 + w];
+                            __builtin_amdgcn_wave_barrier();
+                            __builtin_amdgcn_s_waitcnt(0xc07f);  // (lgkmcnt(0): the stores are done before the reads)
+                            for (int p = 0; p < cn; ++p) {
+                                const double lp[3] = {lds_row[3 * p], lds_row[3 * p + 1], lds_row[3 * p + 2]};
+                                term(lp);
+                            }
+                        }
+                    } else if (__ballot(row != ra) == 0ull) {
+                        uniform_points(row0 + 3 * (int64_t)ra * ns);  // (the wave shares its row)
                     } else {
-                        const int row = light_row(L, B.seed, nr.key, li, 1);
-                        points(row0 + 3 * (int64_t)row * L.num_samples);
+                        // the node's own row (per lane): each point's loads issued two points ahead of its arithmetic
+                        // (the rows are scattered over the 157 MB cache, so a load's latency is a trip to HBM or MALL)
+                        const double* pts = row0 + 3 * (int64_t)row * ns;
+                        double a[3] = {pts[0], pts[1], pts[2]};
+                        const double* q1 = pts + 3 * min(1, ns - 1);
+                        double b[3] = {q1[0], q1[1], q1[2]};
+                        for (int p = 0; p < ns; ++p) {
+                            const double lp[3] = {a[0], a[1], a[2]};
+                            a[0] = b[0];
+                            a[1] = b[1];
+                            a[2] = b[2];
+                            const double* q = pts + 3 * min(p + 2, ns - 1);
+                            b[0] = q[0];
+                            b[1] = q[1];
+                            b[2] = q[2];
+                            term(lp);
+                        }
                     }
                     if (kFactored)
                         for (int k = 0; k < 3; ++k) {
@@ -770,16 +857,51 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
     }
 }
 
+// With a multi-row light (the shipped area-light cache: 65 535 rows of 100 points, 157 MB) every listed node reads
+// the row its shading draw picks, 2.4 KB of the cache per node and a different row in every lane (22 GB fetched per
+// headline-size launch, memory-bound). The list is put in row order first (k_lit_rows lists the nodes densely with
+// their rows, a device radix sort over the rows' 16 bits orders them), so k_shade_lit's waves mostly share one row
+// and read it through the scalar cache. Each lane's result is its own node's (the order changes which nodes share a wave, not what a lane
+// computes).
+__device__ __forceinline__ unsigned lit_total(const unsigned* __restrict__ lcount) {  // (uniform per wave)
+    const int lane = threadIdx.x & 63;
+    unsigned incl = lcount[lane * jit::kMixLine];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    return __shfl(incl, 63, 64);
+}
+
+// the listed nodes densely with their rows of light sort_light (the sort's keys and values)
+__global__ void __launch_bounds__(kBlock) k_lit_rows(DevScene S, Batch B, const ShadowHead* __restrict__ head,
+                                                     const uint32_t* __restrict__ lit, const unsigned* __restrict__ lcount,
+                                                     uint32_t segcap, int sort_light, uint32_t* __restrict__ rows,
+                                                     uint32_t* __restrict__ nodes) {
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned total = lit_total(lcount);
+    if (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) >= total) return;  // (whole waves)
+    const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
+    if (m >= total) return;
+    const uint32_t i = lit[slot];
+    rows[m] = (uint32_t)light_row(S.lights[sort_light], B.seed, head[i].key, sort_light, 1);
+    nodes[m] = i;
+}
+
 // the listed nodes (k_shade); one lane each, the grid sized for every node of the level (4 waves per SIMD asked
 // of the compiler: 128 VGPRs with a few spilled outside the light-point loop, 16.5 -> 15.9 ms per headline
 // frame over its own 3)
 #ifndef FRT_SHADE_WAVES
 #define FRT_SHADE_WAVES 4
 #endif
+// (kRows: the list in light-row order, a multi-row light's row staged per wave in LDS)
+template <bool kRows>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_SHADE_WAVES, 8))) k_shade_lit(DevScene S, Batch B, NodeCols rec,
                                                       const int32_t* __restrict__ counts, Cols<Tri9> surface,
                                                       const uint32_t* __restrict__ lit,
-                                                      const unsigned* __restrict__ lcount, uint32_t segcap) {
+                                                      const unsigned* __restrict__ lcount, uint32_t segcap,
+                                                      const uint32_t* __restrict__ flat) {
     const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
     // the listed total: every lane reads one segment's count (uniform per wave)
     const int lane = threadIdx.x & 63;
@@ -792,12 +914,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     }
     const unsigned total = __shfl(incl, 63, 64);
     if (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) >= total) return;  // (whole waves)
-    const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
-    if (m >= total) return;
-    const int64_t i = (int64_t)lit[slot];
+    int64_t i = 0;
+    if (flat != nullptr) {  // (the list in row order, k_lit_scatter)
+        if (m >= total) return;
+        i = (int64_t)flat[m];
+    } else {
+        const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
+        if (m >= total) return;
+        i = (int64_t)lit[slot];
+    }
     const NodeRec nr = rec.load(i, S.materials);
     double out[12];
-    shade_node(S, B, nr, i, counts, out);
+    if (kRows) {
+        __shared__ double lds_rows[kBlock / 64][3 * kLdsPoints];  // (a multi-row light's row per wave, 3 KB)
+        shade_node(S, B, nr, i, counts, out, lds_rows[threadIdx.x >> 6]);
+    } else {
+        shade_node(S, B, nr, i, counts, out);
+    }
     tri_store(surface, i, out);
 }
 
@@ -1552,6 +1685,15 @@ struct frt_scene_handle {
     // k_shade's list of nodes with light-point work (kShadeSegs segments) and its segment counters
     uint32_t* shade_lit = nullptr;
     int64_t shade_lit_cap = 0;
+    // the lit list in row order (k_shade -> k_lit_rows -> radix sort) for a multi-row light: the listed nodes' rows
+    // (keys, and the sort's alternate buffer), the ordered list (and the unsorted values)
+    int sort_light = -1;               // the first light with more than one cache row (FRT_SHADE_SORT=0: none)
+    uint32_t* lit_row = nullptr;
+    int64_t lit_row_cap = 0;
+    uint32_t* lit_flat = nullptr;
+    int64_t lit_flat_cap = 0;
+    unsigned char* scan_tmp = nullptr;  // (the device sort's temporary storage)
+    int64_t scan_tmp_cap = 0;
     unsigned* shade_lcount = nullptr;
     int64_t shade_lcount_cap = 0;
     unsigned long long* jit_stats = nullptr;  // FRT_JIT_STATS=1: 64 lines x 32 words, [0] live lanes, [1] binary64 re-walks;
@@ -2264,6 +2406,8 @@ int frt_photon_pass_stats(int64_t* out, int n) {
     return 2;
 }
 
+size_t frt_frame_stats_size(void) { return sizeof(frt_frame_stats); }
+
 int frt_upload_phases(double* out, int n) {
     for (int i = 0; i < n && i < 8; ++i) out[i] = t_upload_phases[i];
     return 8;
@@ -2288,11 +2432,20 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     h->device = device;
     frt::DevScene& S = h->S;
     int rc = 0;
-    {  // the scene's identity for the process-wide photon-map sharing (build_photon_maps)
+    if (sc->config.trace_caustic_map || sc->config.trace_global_map) {
+        // the scene's identity for the process-wide photon-map sharing (build_photon_maps), only for scenes that
+        // trace photons: FNV-1a over 8-byte words (the shipped light cache alone is 157 MB)
         uint64_t k = 0xcbf29ce484222325ull;
         auto mix = [&](const void* p, size_t n) {
             const unsigned char* c = (const unsigned char*)p;
-            for (size_t i = 0; i < n; ++i) {
+            size_t i = 0;
+            for (; i + 8 <= n; i += 8) {
+                uint64_t w;
+                std::memcpy(&w, c + i, 8);
+                k ^= w;
+                k *= 0x100000001b3ull;
+            }
+            for (; i < n; ++i) {
                 k ^= c[i];
                 k *= 0x100000001b3ull;
             }
@@ -2555,6 +2708,12 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
     S.cam = sc->camera;
     S.cfg = sc->config;
     h->host_lights.assign(sc->lights, sc->lights + sc->num_lights);
+    {  // the lit list in row order for the first multi-row area / circle light (FRT_SHADE_SORT=0: never)
+        const char* e = std::getenv("FRT_SHADE_SORT");
+        h->sort_light = -1;
+        for (int l = 0; l < sc->num_lights && h->sort_light < 0 && !(e && std::atoi(e) == 0); ++l)
+            if (sc->lights[l].rows > 1 && sc->lights[l].num_samples > 0) h->sort_light = l;
+    }
     // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
     // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L
     // has codes up to 2^(L+1) - 1, so L <= 11. The reference accepts any length; deeper recursion
@@ -2688,6 +2847,9 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->counters));
     hip_ignore(hipFree(h->shade_lit));
     hip_ignore(hipFree(h->shade_lcount));
+    hip_ignore(hipFree(h->lit_row));
+    hip_ignore(hipFree(h->lit_flat));
+    hip_ignore(hipFree(h->scan_tmp));
     hip_ignore(hipFree(h->mixed));
     hip_ignore(hipFree(h->tlist));
     hip_ignore(hipFree(h->slist));
@@ -2790,7 +2952,7 @@ static void collect_timings(frt_scene_handle* h, frt_frame_stats* st) {
         if (m.slot < 8) {
             st->kernel_ms[m.slot] += ms;
             st->kernel_launches[m.slot] += 1;
-        } else {
+        } else if (m.slot < 24) {
             st->sub_ms[m.slot - 8] += ms;
             st->sub_launches[m.slot - 8] += 1;
         }
@@ -3688,8 +3850,8 @@ static int build_photon_map(frt_scene_handle* h, const std::vector<frt::StoredPh
 // process share them: the first handle to ask traces them on its device and prepares the host arrays (the
 // balance, the grid, the records: host work on the process's CPUs), the others wait for that and upload the
 // same arrays (render_multi over N devices: one photon pass, not N on the same CPUs). Entries are keyed by
-// the scene content's hash and the seed; the last two stay (in-flight users hold their own reference), so a
-// later call with the same scene and seed (render_multi again, another handle) uploads them without a pass.
+// the scene content's hash and the seed and held weakly: the maps' host arrays (~130 MB per 1M-photon map) live
+// while some handle of that (scene, seed) still uploads them, and are freed after the last one.
 struct SharedMaps {
     std::mutex mu;
     std::condition_variable cv;
@@ -3698,7 +3860,7 @@ struct SharedMaps {
     uint64_t photons[2] = {0, 0};
 };
 static std::mutex g_maps_mu;
-static std::vector<std::pair<std::pair<uint64_t, uint64_t>, std::shared_ptr<SharedMaps>>> g_maps;  // newest last
+static std::vector<std::pair<std::pair<uint64_t, uint64_t>, std::weak_ptr<SharedMaps>>> g_maps;
 
 
 // trace_photons for one render seed: caustic map 0, global map 1
@@ -3713,19 +3875,39 @@ static int build_photon_maps(frt_scene_handle* h, uint64_t seed) {
     if (share) {
         const std::pair<uint64_t, uint64_t> key(h->scene_key, seed);
         std::lock_guard<std::mutex> lk(g_maps_mu);
-        for (auto& e : g_maps)
-            if (e.first == key) sm = e.second;
+        for (size_t i = 0; i < g_maps.size();) {  // (expired entries out)
+            if (g_maps[i].second.expired()) {
+                g_maps.erase(g_maps.begin() + (ptrdiff_t)i);
+                continue;
+            }
+            if (g_maps[i].first == key) sm = g_maps[i].second.lock();
+            ++i;
+        }
         if (sm) {
             producer = false;
         } else {
             sm = std::make_shared<SharedMaps>();
             g_maps.emplace_back(key, sm);
-            if (g_maps.size() > 2) g_maps.erase(g_maps.begin());  // (1M-photon maps: ~130 MB of host arrays each)
         }
     } else {
         sm = std::make_shared<SharedMaps>();
     }
     if (producer) {
+        // every exit from the producer (an exception included) leaves a final state, so no consumer waits forever
+        struct Settle {
+            SharedMaps* m;
+            ~Settle() {
+                bool notify = false;
+                {
+                    std::lock_guard<std::mutex> lk(m->mu);
+                    if (m->state == 0) {
+                        m->state = -1;
+                        notify = true;
+                    }
+                }
+                if (notify) m->cv.notify_all();
+            }
+        } settle{sm.get()};
         int rc = 0;
         for (int m = 0; m < 2 && rc == 0; ++m) {
             const auto t0 = std::chrono::steady_clock::now();
@@ -3754,7 +3936,7 @@ static int build_photon_maps(frt_scene_handle* h, uint64_t seed) {
         if (rc) {  // (a later frame may try again)
             std::lock_guard<std::mutex> lk(g_maps_mu);
             for (size_t i = 0; i < g_maps.size(); ++i)
-                if (g_maps[i].second == sm) {
+                if (g_maps[i].second.lock() == sm) {
                     g_maps.erase(g_maps.begin() + (ptrdiff_t)i);
                     break;
                 }
@@ -4045,16 +4227,57 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 if (split)
                     FRT_HIP(hipMemsetAsync(h->shade_lcount, 0, (size_t)kShadeSegs * jit::kMixLine * sizeof(unsigned),
                                            h->stream));
+                // the row sort (multi-row light): row counts beside the list, then the list in row order
+                const bool sorted = split && h->sort_light >= 0;
+                const int nrows = sorted ? std::max(1, h->host_lights[(size_t)h->sort_light].rows) : 0;
+                int row_bits = 1;
+                while (row_bits < 32 && (1ll << row_bits) < nrows) ++row_bits;
+                if (sorted) {
+                    const int64_t lcap = (int64_t)segcap * kShadeSegs;
+                    if (grow(&h->lit_row, h->lit_row_cap, 2 * lcap) || grow(&h->lit_flat, h->lit_flat_cap, 2 * lcap))
+                        return -1;
+                }
                 if (shade_lazy(h))
                     hipLaunchKernelGGL(k_shade<true>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
                                        L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap);
                 else
                     hipLaunchKernelGGL(k_shade<false>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
                                        L.counts, L.surface, split ? h->shade_lit : nullptr, h->shade_lcount, segcap);
+                if (sorted) {
+                    KTimer ts(h, st, 16);  // (k_lit_rows + the radix sort, sub_ms["k_lit_sort"])
+                    const int64_t lcap = (int64_t)segcap * kShadeSegs;
+                    uint32_t *keys = h->lit_row, *keys2 = h->lit_row + lcap, *vals = h->lit_flat + lcap;
+                    hipLaunchKernelGGL(k_lit_rows, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.head,
+                                       h->shade_lit, h->shade_lcount, segcap, h->sort_light, keys, vals);
+                    // (the listed count on the host: the sort's size)
+                    std::vector<unsigned> lc((size_t)kShadeSegs * jit::kMixLine);
+                    FRT_HIP(hipMemcpyAsync(lc.data(), h->shade_lcount, lc.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
+                                           h->stream));
+                    FRT_HIP(hipStreamSynchronize(h->stream));
+                    int64_t listed = 0;
+                    for (int sgi = 0; sgi < kShadeSegs; ++sgi) listed += lc[(size_t)sgi * jit::kMixLine];
+                    if (st != nullptr) st->lit_nodes += (uint64_t)listed;
+                    if (listed > 0) {
+                        size_t tmp_bytes = 0;
+                        FRT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, h->lit_flat,
+                                                                   (int)listed, 0, row_bits, h->stream));
+                        if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
+                        FRT_HIP(hipcub::DeviceRadixSort::SortPairs((void*)h->scan_tmp, tmp_bytes, keys, keys2, vals,
+                                                                   h->lit_flat, (int)listed, 0, row_bits, h->stream));
+                    }
+                }
+                if (split && st != nullptr && !sorted) {  // (the stats frame: the listed count, frt_frame_stats.lit_nodes)
+                    std::vector<unsigned> lc((size_t)kShadeSegs * jit::kMixLine);
+                    FRT_HIP(hipMemcpyAsync(lc.data(), h->shade_lcount, lc.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
+                                           h->stream));
+                    FRT_HIP(hipStreamSynchronize(h->stream));
+                    for (int sgi = 0; sgi < kShadeSegs; ++sgi) st->lit_nodes += lc[(size_t)sgi * jit::kMixLine];
+                }
                 if (split) {
                     KTimer tl(h, st, 15);  // (inside the shade slot: k_shade_lit alone, sub_ms[7])
-                    hipLaunchKernelGGL(k_shade_lit, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec,
-                                       L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap);
+                    hipLaunchKernelGGL(sorted ? k_shade_lit<true> : k_shade_lit<false>, dim3(grid_for(n)), dim3(kBlock), 0,
+                                       h->stream, h->S, B, L.rec, L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap,
+                                       sorted ? (const uint32_t*)h->lit_flat : nullptr);
                 }
                 FRT_HIP(hipGetLastError());
             }

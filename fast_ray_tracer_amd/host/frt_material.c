@@ -4,7 +4,7 @@
  * Material defaults restate reference src/material/material.c:7-31 (white
  * Ka/Kd/Ks, black Tf/Ke/refl, Ns 200, Ni 1, casts shadows). Patterns are plain
  * data here (type + colors + transform + child links); the evaluation
- * functions live on the device (csrc/frt_trace.hip) and in the CPU oracle.
+ * functions live on the device (csrc/frt_shade.hpp) and in the CPU oracle.
  * Reference-count semantics (pattern.c:633-700, material.c:102-125) are kept
  * so that generated main() code frees exactly what the reference frees.
  */

@@ -36,17 +36,17 @@ class FrameStats(ctypes.Structure):
                 ("shadow_kernel_bytes", ctypes.c_double), ("gather_rays", ctypes.c_uint64),
                 ("photons", ctypes.c_uint64 * 2), ("photon_ms", ctypes.c_double),
                 ("shadow_jit", ctypes.c_int32), ("photon_pass", ctypes.c_int32),
-                ("sub_ms", ctypes.c_double * 8), ("sub_launches", ctypes.c_uint64 * 8),
+                ("sub_ms", ctypes.c_double * 16), ("sub_launches", ctypes.c_uint64 * 16),
                 ("shadow_rays_walked", ctypes.c_uint64), ("shadow_tile_pairs", ctypes.c_uint64),
                 ("shadow_tile_mixed", ctypes.c_uint64), ("shadow_pairs", ctypes.c_uint64),
                 ("shadow_pairs_mixed", ctypes.c_uint64), ("shadow_sub_pairs", ctypes.c_uint64),
                 ("shadow_sub_mixed", ctypes.c_uint64), ("shadow_subtile_pairs", ctypes.c_uint64),
-                ("shadow_subtile_mixed", ctypes.c_uint64)]
+                ("shadow_subtile_mixed", ctypes.c_uint64), ("lit_nodes", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         names = ["trace", "shadow", "shade", "combine", "resolve", "trace_primary", "prepare", "gi"]
         subs = ["frt_jit_beam", "frt_jit_shadow", "k_gather_est", "k_gather_hit", "frt_jit_tile", "frt_jit_sub",
-                "frt_jit_subtile", "k_shade_lit"]
+                "frt_jit_subtile", "k_shade_lit", "k_lit_sort"]
         return {
             "primary_rays": int(self.primary_rays), "secondary_rays": int(self.secondary_rays),
             "shadow_rays": int(self.shadow_rays), "pruned_secondary": int(self.pruned_secondary),
@@ -64,7 +64,7 @@ class FrameStats(ctypes.Structure):
             "shadow_pairs": int(self.shadow_pairs), "shadow_pairs_mixed": int(self.shadow_pairs_mixed),
             "shadow_sub_pairs": int(self.shadow_sub_pairs), "shadow_sub_mixed": int(self.shadow_sub_mixed),
             "shadow_subtile_pairs": int(self.shadow_subtile_pairs),
-            "shadow_subtile_mixed": int(self.shadow_subtile_mixed),
+            "shadow_subtile_mixed": int(self.shadow_subtile_mixed), "lit_nodes": int(self.lit_nodes),
         }
 
 
@@ -103,6 +103,10 @@ def host_lib(auto_build: bool = False) -> ctypes.CDLL:
         lib.frt_scene_release.argtypes = [vp]
         lib.frt_encode_ppm.restype = ctypes.c_size_t
         lib.frt_encode_ppm.argtypes = [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, vp, ctypes.c_size_t]
+        lib.frt_frame_stats_size.restype = ctypes.c_size_t
+        if lib.frt_frame_stats_size() != ctypes.sizeof(FrameStats):  # (a stale library against this mirror)
+            raise RuntimeError("frt: frt_frame_stats is %d bytes in %s, runtime.py FrameStats %d: rebuild"
+                               % (lib.frt_frame_stats_size(), build.DEVICE_LIB, ctypes.sizeof(FrameStats)))
         _host = lib
         return lib
 

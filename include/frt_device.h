@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 2u
+#define FRT_ABI_VERSION 3u  /* 3: frt_frame_stats grew the beam-stage counters (round 4) */
 
 /* node kinds: same numbering as the reference's enum shape_enum (shapes.h:16-27) */
 enum frt_node_type {
@@ -219,9 +219,10 @@ typedef struct frt_frame_stats {
     /* kernels inside the slots above (HIP events around each launch on the engine stream):
        0 frt_jit_beam / frt_jit_beam_list (node pair kernel), 1 frt_jit_shadow (per-ray kernel), 2 k_gather_est,
        3 k_gather_hit, 4 frt_jit_tile (tile pair kernel), 5 frt_jit_sub (sub-part pair kernel), 6 frt_jit_subtile
-       (sub-tile pair kernel), 7 k_shade_lit (the shading of the path nodes some light reaches) */
-    double sub_ms[8];
-    uint64_t sub_launches[8];
+       (sub-tile pair kernel), 7 k_shade_lit (the shading of the path nodes some light reaches), 8 k_lit_scan +
+       k_lit_scatter (the lit list in light-row order, multi-row lights); 9-15 unused */
+    double sub_ms[16];
+    uint64_t sub_launches[16];
     uint64_t shadow_rays_walked;  /* shadow rays walked one by one; the rest of shadow_rays were resolved
                                      (exactly, for every ray) per (node, light part) by frt_jit_beam */
     /* the scene-specialised pair kernels' work this frame (0 without them) */
@@ -233,10 +234,16 @@ typedef struct frt_frame_stats {
     uint64_t shadow_sub_mixed;    /* of those, the ones left mixed */
     uint64_t shadow_subtile_pairs; /* (sub-tile, light sub-part) beams of those tested by frt_jit_subtile */
     uint64_t shadow_subtile_mixed; /* of those, the ones whose nodes frt_jit_beam_list tested */
+    uint64_t lit_nodes;           /* path nodes some light sample reaches (k_shade_lit's lanes); counted per frame
+                                     when stats are asked for */
 } frt_frame_stats;
 
 /* number of HIP devices visible (0 when no GPU) */
 int frt_device_count(void);
+
+/* sizeof(frt_frame_stats) as this library was built: a caller's mirror of the struct (runtime.py FrameStats)
+ * checks its size against it before passing one in (no device needed) */
+size_t frt_frame_stats_size(void);
 
 /* message of the last failing call on this thread */
 const char *frt_last_error(void);

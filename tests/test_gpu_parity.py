@@ -177,7 +177,8 @@ def test_render_multi_shares_photon_maps_across_devices(built):
     """render_multi over several devices of one process traces and balances the photon maps once (frt_engine.hip
     build_photon_maps: the first handle traces, the others upload the same host arrays): the GI canvas over two
     and three handles on device 0 equals the canvas with every handle tracing its own maps (FRT_SHARE_PHOTONS=0)
-    bit for bit, and the counters show the passes traced and shared."""
+    bit for bit, and the counters show the passes traced and shared (the maps' host arrays are held only while a
+    handle of the call still uploads them, so a later call with the same seed traces again)."""
     import ctypes
     from fast_ray_tracer_amd.runtime import host_lib, render_multi
     lib = host_lib()
@@ -199,7 +200,8 @@ def test_render_multi_shares_photon_maps_across_devices(built):
         del os.environ["FRT_SHARE_PHOTONS"]
         two = render_multi(sc, devices="0,0")  # one pass for both handles
         t2, s2 = passes()
-        three = render_multi(sc, devices="0,0,0")  # the same scene and seed again: the maps are kept
+        three = render_multi(sc, devices="0,0,0")  # the same scene and seed again: traced anew (the host arrays
+        # are freed after the last handle of a call uploads them), shared by the three handles
         t3, s3 = passes()
     finally:
         for k, v in saved.items():
@@ -209,7 +211,7 @@ def test_render_multi_shares_photon_maps_across_devices(built):
                 os.environ[k] = v
     assert (t1 - t0, s1 - s0) == (2, 0), (t0, s0, t1, s1)
     assert (t2 - t1, s2 - s1) == (1, 1), (t1, s1, t2, s2)
-    assert (t3 - t2, s3 - s2) == (0, 3), (t2, s2, t3, s3)
+    assert (t3 - t2, s3 - s2) == (1, 2), (t2, s2, t3, s3)
     assert np.isfinite(own).all() and own[:, :, :3].max() > 0
     assert np.array_equal(own, two) and np.array_equal(own, three)
 
@@ -274,6 +276,8 @@ def test_jit_compiled_once_and_cached_on_disk(built, tmp_path):
     # the record only (the process's first module load and allocations vary by box: bench.py reports the
     # phases of a second process's render_multi, render_multi_phases_second_process)
     print("second process: cold %.1f ms, warm %.1f ms" % (second["cold_ms"], second["warm_ms"]))
+    # a generous bound all the same (a regression in module loads, allocations or per-upload work shows here)
+    assert second["cold_ms"] <= second["warm_ms"] + 1000.0, second
     # a corrupt cached object (its payload checksum fails) is dropped and compiled again, and renders
     co = [f for f in os.listdir(tmp_path / "co") if f.endswith(".co")]
     assert len(co) == 1
@@ -395,3 +399,17 @@ def test_math_core_sequences_bit_identical(built):
     lib.frt_math_selftest.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     for seed in (1, 0x5eed):
         assert lib.frt_math_selftest(1 << 22, seed) == 0
+
+
+@pytest.mark.parametrize("name,rows", [("cornell_shipped_48_4x4", None), ("cornell_gi_24", None),
+                                       ("cornell_shipped_1920x1080_8x8", (520, 528))])
+def test_row_sorted_shading_equals_list_order(built, name, rows):
+    """With a multi-row light (the shipped 65 535-row cache) the lit nodes are shaded in the order of the light row
+    their shading draw picks (k_lit_scan / k_lit_scatter), so a wave mostly shares one row and reads it through the
+    scalar cache. Each lane still shades its own node, so the canvas equals the one in list order (FRT_SHADE_SORT=0)
+    bit for bit: the shipped direct configuration, a GI one and a band of the shipped 1920x1080x64 frame."""
+    kw = {} if rows is None else {"row_begin": rows[0], "row_end": rows[1]}
+    sorted_ = _render_env(name, {"FRT_SHADE_SORT": "1"}, **kw)
+    plain = _render_env(name, {"FRT_SHADE_SORT": "0"}, **kw)
+    assert np.isfinite(sorted_).all() and sorted_[:, :, :3].max() > 0
+    assert np.array_equal(sorted_, plain)

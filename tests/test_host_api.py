@@ -30,6 +30,15 @@ def test_device_library_exports_abi(built):
     assert not missing, missing
 
 
+def test_frame_stats_layout_matches_runtime_mirror(built):
+    """runtime.py's ctypes FrameStats mirrors include/frt_device.h frt_frame_stats: the library reports the struct's
+    size as built (frt_frame_stats_size) and the mirror has the same."""
+    from fast_ray_tracer_amd.runtime import FrameStats
+    lib = ctypes.CDLL(built.DEVICE_LIB)
+    lib.frt_frame_stats_size.restype = ctypes.c_size_t
+    assert lib.frt_frame_stats_size() == ctypes.sizeof(FrameStats)
+
+
 def test_device_count_without_gpu_is_safe(built):
     lib = ctypes.CDLL(built.DEVICE_LIB)
     lib.frt_device_count.restype = ctypes.c_int
@@ -58,8 +67,10 @@ def test_host_library_exports_reference_api(built):
     assert not missing, missing
 
 
-@pytest.mark.parametrize("main_c", sorted(glob.glob(os.path.join(GOLDEN, "scenes", "*.c")))[:6])
+@pytest.mark.parametrize("main_c", sorted(glob.glob(os.path.join(GOLDEN, "scenes", "*.c"))))
 def test_generated_main_compiles_unchanged(built, tmp_path, main_c):
+    """Every generated main.c of the golden set links as an executable against libfrt_host (render_multi on the
+    GPU), unchanged."""
     exe = tmp_path / "scene"
     built.build_scene_executable(main_c, str(exe))
     assert exe.exists()

@@ -12,6 +12,7 @@ for v in "$@"; do
   python3 -c "
 import json,sys
 d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); sp=d['shadow_pass']
-print('%-40s ms %8.3f shadow %7.3f shade %6.3f prepare %6.3f | %s | node_pairs %s walked %s' % (sys.argv[2], d['ms_per_step'], d['kernel_ms_per_frame']['shadow'], d['kernel_ms_per_frame']['shade'], d['kernel_ms_per_frame']['prepare'], ' '.join('%s %.2f' % (k[8:], v) for k, v in sp['kernels_ms_per_frame'].items()), sp['node_pairs'], sp['shadow_rays_walked_per_ray']))
+sub = d['sub_ms_per_frame']
+print('%-40s ms %8.3f shadow %7.3f shade %6.3f (lit %6.3f sort %5.3f) prepare %6.3f | %s | node_pairs %s walked %s lit %s' % (sys.argv[2], d['ms_per_step'], d['kernel_ms_per_frame']['shadow'], d['kernel_ms_per_frame']['shade'], sub.get('k_shade_lit', 0), sub.get('k_lit_sort', 0), d['kernel_ms_per_frame']['prepare'], ' '.join('%s %.2f' % (k[8:], v) for k, v in sp['kernels_ms_per_frame'].items()), sp['node_pairs'], sp['shadow_rays_walked_per_ray'], d.get('lit_nodes_per_frame')))
 " gpurun_out/ab_${label}.json "$v" | tee -a $out
 done
