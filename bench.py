@@ -18,6 +18,8 @@ reference would cast, counted by the oracle: zero-weight secondary subtrees
 included) are reported beside it.
 
 Also on the same JSON line:
+  shipped          the shipped direct-lighting configuration (cornell_box.yml's 65 535-row jittered light cache, GI
+                   off) at 1920x1080x64: --shipped-steps frames
   gi               the shipped GI configuration (BASELINE configs[4]: 1M photons per map,
                    8x8 final gather, k = 200) at 1920x1080x64: --gi-steps frames, each with a
                    new seed so photon tracing + map build run inside the timed region
@@ -53,6 +55,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 ASSETS = os.path.join(GOLDEN, "assets")
 DEFAULT_SCENE = "cornell_direct_1920x1080_8x8"
 GI_SCENE = "cornell_gi_1920x1080_8x8"
+SHIPPED_SCENE = "cornell_shipped_1920x1080_8x8"
 CPU_SAMPLE_SCENE = "cornell_direct_240x135_8x8"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 2 cycles (SIMD32; binary64
@@ -408,6 +411,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gi-steps", type=int, default=1, help="timed GI frames (0: skip the GI line)")
+    ap.add_argument("--shipped-steps", type=int, default=3,
+                    help="timed frames of the shipped light configuration (0: skip the shipped line)")
     ap.add_argument("--scene", default=DEFAULT_SCENE)
     # camera samples per batch on the resident handle: the whole headline frame (frt_render_params.batch_samples; the
     # engine's own default, 2^23, suits one-shot calls such as render_multi, which allocate per call: DESIGN.md §2)
@@ -540,6 +545,48 @@ def main():
     renderer.close()
     del shard
 
+    # ---- the shipped direct-lighting configuration: cornell_box.yml's own 65 535-row jittered light cache, GI off, at
+    # the headline size (each path node draws its own cache rows: statistical parity, tests/test_gpu_stochastic.py and
+    # the fixed-seed bit-identity of every shadow stage, tests/test_jit.py) ----
+    shipped = None
+    if args.shipped_steps > 0 and args.scene == DEFAULT_SCENE:
+        sscene = scene_of(SHIPPED_SCENE)
+        srend = GpuRenderer(sscene, device=local_rank)
+        sshard = torch.zeros((shard_capacity(world, sscene.height), sscene.width, 4), dtype=torch.float64, device="cuda")
+        frame(srend, sshard, sscene.height)  # (untimed warmup: level state allocated)
+        sync()
+        s0 = time.perf_counter()
+        for _ in range(args.shipped_steps):
+            frame(srend, sshard, sscene.height)
+        sync()
+        s_elapsed = time.perf_counter() - s0
+        sst, _ = frame(srend, sshard, sscene.height, stats=True)
+        sd = sst.as_dict()
+        if sd["errors"]:
+            raise RuntimeError("engine reported errors in the shipped frame: %s" % sd)
+        st_t = torch.tensor([s_elapsed], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(st_t, op=dist.ReduceOp.MAX)
+        s_ms = 1e3 * float(st_t.item()) / args.shipped_steps
+        s_rays = (sd["primary_rays"] + sd["secondary_rays"] + sd["shadow_rays"]) * world
+        s_ref = reference_rays(SHIPPED_SCENE)
+        shipped = {"workload": SHIPPED_SCENE, "width": sscene.width, "height": sscene.height, "spp": sscene.spp,
+                   "steps": args.shipped_steps, "ms_per_step": round(s_ms, 3),
+                   "value": round(s_rays / (s_ms * 1e-3) / 1e6, 3), "unit": "Mrays/s",
+                   "reference_equivalent_mrays_s": round(s_ref / (s_ms * 1e-3) / 1e6, 3) if s_ref else None,
+                   "kernel_ms_per_frame": {k: round(v, 3) for k, v in sd["kernel_ms"].items()},
+                   "sub_ms_per_frame": {k: round(v, 3) for k, v in sd.get("sub_ms", {}).items()},
+                   "lit_nodes_per_frame": sd.get("lit_nodes"),
+                   "shadow_pass": {"tile_pairs": sd.get("shadow_tile_pairs"), "tile_pairs_mixed": sd.get("shadow_tile_mixed"),
+                                   "tile_sub_pairs": sd.get("shadow_sub_pairs"),
+                                   "tile_sub_pairs_mixed": sd.get("shadow_sub_mixed"),
+                                   "shadow_rays_per_frame": sd["shadow_rays"],
+                                   "shadow_rays_walked_per_ray": sd.get("shadow_rays_walked")},
+                   "data": "reference codegen main.c of scenes/cornell_box as shipped (65535-row jittered light cache, "
+                           "camera jitter off) with GI off, at 1920x1080x64"}
+        srend.close()
+        del sshard
+
     # ---- GI (configs[4]): fresh photon maps inside every timed frame ----
     gi = None
     if args.gi_steps > 0:
@@ -641,6 +688,8 @@ def main():
             "roofline_shadow_pass": roof_shadow,
         }
         out.update(rm)
+        if shipped is not None:
+            out["shipped"] = shipped
         if gi is not None:
             out["gi"] = gi
         if proxy is not None:

@@ -2408,6 +2408,17 @@ int frt_photon_pass_stats(int64_t* out, int n) {
 
 size_t frt_frame_stats_size(void) { return sizeof(frt_frame_stats); }
 
+int frt_device_warmup(int device) {
+    if (hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    hip_ignore(hipFree(nullptr));  // (creates the context)
+    void* p = nullptr;
+    if (hipMalloc(&p, 1 << 20) == hipSuccess) hip_ignore(hipFree(p));
+    return 0;
+}
+
 int frt_upload_phases(double* out, int n) {
     for (int i = 0; i < n && i < 8; ++i) out[i] = t_upload_phases[i];
     return 8;
@@ -2536,15 +2547,9 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
             // (the closest-hit kernel writes n1 = n2 = 1: scenes with refractive indices other than one keep k_trace)
             h->jit_trace = sc->config.all_ni_one ? fns.trace : nullptr;
             h->subtile = fns.subtile ? frt_jit_subtile_size() : 0;
-            {
-                // multi-row lights (the shipped area-light cache): the sub-tile stage decides few of the (tile, sample)
-                // pairs the sub-part stage leaves — the sample's point lies anywhere in its light cell for the sub-tile's
-                // nodes — so it runs only when FRT_JIT_SUBTILE asks for it (round 5, profiles/r05_ab_nodebeam.txt: it
-                // cut the shipped frame's per-ray lanes by 11 % for 6.5 ms; without it 76.4 -> 72.1 ms)
-                bool multi = false;
-                for (int l = 0; l < sc->num_lights; ++l) multi = multi || sc->lights[l].rows > 1;
-                if (multi && !std::getenv("FRT_JIT_SUBTILE")) h->subtile = 0;
-            }
+            // (multi-row lights get no sub-tile kernel unless FRT_JIT_SUBTILE asks for one, frt_jit_shadow_source: the
+            // stage cut the shipped frame's per-ray lanes by 11 % for 6.5 ms; without it 76.4 -> 72.1 ms,
+            // profiles/r05_ab_nodebeam.txt)
             if (h->jit_shadow) {
                 h->redo_cap = 1u << 20;
                 void* p = nullptr;

@@ -238,15 +238,32 @@ static double g_rm_phases[16];
 /*
  * Diagnostics: the phases of the last render_multi, in ms: out[0] flatten, [1] upload (the slowest device),
  * [2..9] that device's frt_upload_phases, [10] render of its rows incl. the copy to host memory (the slowest
- * device), [11] placing the rows into the canvas, [12] release, [13] total. Writes min(n, 14); returns 14.
+ * device), [11] placing the rows into the canvas, [12] release, [13] total, [14] the devices' runtime
+ * initialisation (frt_device_warmup, on threads beside the flatten), [15] the wait for it after the flatten.
+ * Writes min(n, 16); returns 16.
  */
 int
 frt_render_multi_phases(double *out, int n)
 {
-    for (int i = 0; i < n && i < 14; ++i) {
+    for (int i = 0; i < n && i < 16; ++i) {
         out[i] = g_rm_phases[i];
     }
-    return 14;
+    return 16;
+}
+
+typedef struct {
+    int device;
+    double ms;
+} warmup_job;
+
+static void *
+warmup_worker(void *arg)
+{
+    warmup_job *j = (warmup_job *)arg;
+    const double t0 = now_ms();
+    frt_device_warmup(j->device);
+    j->ms = now_ms() - t0;
+    return NULL;
 }
 
 /*
@@ -264,24 +281,51 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     const double rm0 = now_ms();
     memset(g_rm_phases, 0, sizeof(g_rm_phases));
     const size_t width = cam != NULL ? cam->hsize : 1, height = cam != NULL ? cam->vsize : 1;
+    /* (the canvas is zeroed only where a failure leaves it unwritten: a successful render writes every pixel) */
     Canvas c = canvas_alloc(width, height, false, NULL);
-    memset(c->arr, 0, width * height * sizeof(Color));
     int dev[FRT_MAX_RENDER_DEVICES];
     char err[512];
     frt_scene fs;
     g_render_error[0] = '\0';
-    const int flat_rc = host_flatten(cam, w, usteps, vsteps, jitter, &fs);
-    g_rm_phases[0] = now_ms() - rm0;
-    if (flat_rc) {
-        fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", g_host_error);
-        snprintf(g_render_error, sizeof(g_render_error), "%s", g_host_error);
-        return c;
-    }
     const int n = render_devices(dev, FRT_MAX_RENDER_DEVICES, err, sizeof(err));
     if (n < 0) {
         fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", err);
         snprintf(g_render_error, sizeof(g_render_error), "%s", err);
-        frt_flat_scene_free(&fs);
+        memset(c->arr, 0, width * height * sizeof(Color));
+        return c;
+    }
+    /* the devices' HIP contexts are created on threads of their own while this thread flattens the scene (a
+     * process's first context costs more than the flatten; frt_device_warmup) */
+    warmup_job wj[FRT_MAX_RENDER_DEVICES];
+    pthread_t wt[FRT_MAX_RENDER_DEVICES];
+    int nw = 0;
+    for (int k = 0; k < n; ++k) {
+        int seen = 0;
+        for (int q = 0; q < nw; ++q) {
+            seen = seen || wj[q].device == dev[k];
+        }
+        if (seen) {
+            continue;
+        }
+        wj[nw].device = dev[k];
+        wj[nw].ms = 0.0;
+        if (pthread_create(&wt[nw], NULL, warmup_worker, &wj[nw]) == 0) {
+            ++nw;
+        }
+    }
+    const double fl0 = now_ms();
+    const int flat_rc = host_flatten(cam, w, usteps, vsteps, jitter, &fs);
+    g_rm_phases[0] = now_ms() - fl0;
+    const double wj0 = now_ms();
+    for (int q = 0; q < nw; ++q) {
+        pthread_join(wt[q], NULL);
+        g_rm_phases[14] = wj[q].ms > g_rm_phases[14] ? wj[q].ms : g_rm_phases[14];
+    }
+    g_rm_phases[15] = now_ms() - wj0;
+    if (flat_rc) {
+        fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", g_host_error);
+        snprintf(g_render_error, sizeof(g_render_error), "%s", g_host_error);
+        memset(c->arr, 0, width * height * sizeof(Color));
         return c;
     }
     const char *seed_env = getenv("FRT_SEED");
@@ -301,7 +345,8 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
         j->width = (int64_t)width;
         j->seed = seed;
         j->want_stats = stats_path != NULL;
-        j->rows = (double *)malloc((size_t)(nrows > 0 ? nrows : 1) * width * 4 * sizeof(double));
+        /* one device renders every row in order: straight into the canvas (a Color is 4 doubles) */
+        j->rows = n == 1 ? (double *)c->arr : (double *)malloc((size_t)(nrows > 0 ? nrows : 1) * width * 4 * sizeof(double));
         if (j->rows == NULL) {
             failed = 1;
             snprintf(err, sizeof(err), "out of host memory");
@@ -352,7 +397,7 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
         for (int k = 0; k < n; ++k) {
             const device_job *j = &jobs[k];
             int64_t i = 0;
-            for (int64_t r = k; r < (int64_t)height; r += n, ++i) {
+            for (int64_t r = k; n > 1 && r < (int64_t)height; r += n, ++i) {
                 memcpy(c->arr + (size_t)r * width, j->rows + (size_t)i * width * 4, width * sizeof(Color));
             }
             total.primary_rays += j->st.primary_rays;
@@ -371,8 +416,9 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     } else {
         fprintf(stderr, "frt: render_multi failed: %s\n", err);
         snprintf(g_render_error, sizeof(g_render_error), "%s", err[0] ? err : "failed");
+        memset(c->arr, 0, width * height * sizeof(Color));
     }
-    for (int k = 0; jobs != NULL && k < n; ++k) {
+    for (int k = 0; jobs != NULL && n > 1 && k < n; ++k) {
         free(jobs[k].rows);
     }
     free(jobs);

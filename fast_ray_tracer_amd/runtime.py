@@ -249,7 +249,8 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
 
 RENDER_MULTI_PHASES = ("flatten", "upload", "upload.device_select", "upload.scene_buffers", "upload.walk_records_meshes",
                        "upload.jit_source", "upload.jit_code_object", "upload.jit_module_load", "upload.rest",
-                       "upload.total", "render_rows_and_copy", "place_rows", "release", "total")
+                       "upload.total", "render_rows_and_copy", "place_rows", "release", "total", "device_warmup",
+                       "device_warmup_wait")
 
 
 def render_multi_phases() -> dict:
@@ -259,8 +260,8 @@ def render_multi_phases() -> dict:
     lib = host_lib()
     lib.frt_render_multi_phases.restype = ctypes.c_int
     lib.frt_render_multi_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    out = (ctypes.c_double * 14)()
-    lib.frt_render_multi_phases(out, 14)
+    out = (ctypes.c_double * 16)()
+    lib.frt_render_multi_phases(out, 16)
     return {k: round(float(v), 3) for k, v in zip(RENDER_MULTI_PHASES, out)}
 
 

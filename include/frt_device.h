@@ -241,6 +241,10 @@ typedef struct frt_frame_stats {
 /* number of HIP devices visible (0 when no GPU) */
 int frt_device_count(void);
 
+/* create the HIP runtime's context on `device` ahead of use (render_multi runs it on a thread of its own per device
+ * while it flattens the scene); returns 0, or -1 when the device cannot be set */
+int frt_device_warmup(int device);
+
 /* sizeof(frt_frame_stats) as this library was built: a caller's mirror of the struct (runtime.py FrameStats)
  * checks its size against it before passing one in (no device needed) */
 size_t frt_frame_stats_size(void);

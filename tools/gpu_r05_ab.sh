@@ -8,7 +8,7 @@ out=gpurun_out/ab_${label}.txt
 : > $out
 for v in "$@"; do
   env $v timeout -k 10 300 python -u bench.py --scene $sc --steps 5 --warmup 1 --gi-steps 0 --no-cpu-baseline --no-render-multi \
-    --no-scaling-proxy > gpurun_out/ab_${label}.json 2> gpurun_out/ab_${label}.err || { tail -20 gpurun_out/ab_${label}.err; exit 1; }
+    --no-scaling-proxy --shipped-steps 0 > gpurun_out/ab_${label}.json 2> gpurun_out/ab_${label}.err || { tail -20 gpurun_out/ab_${label}.err; exit 1; }
   python3 -c "
 import json,sys
 d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); sp=d['shadow_pass']

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="--scene $SC --gi-steps 0 --no-cpu-baseline --no-render-multi --no-scaling-proxy $*"
+B="--scene $SC --gi-steps 0 --no-cpu-baseline --no-render-multi --no-scaling-proxy --shipped-steps 0 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/kt" -o run -- \
     python3 "$R/bench.py" --steps 3 --warmup 1 $B > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" || exit $?
 KRE=$(echo $KS | tr ' ' '|')
