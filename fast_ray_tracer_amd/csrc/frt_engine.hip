@@ -1623,6 +1623,39 @@ __global__ void __launch_bounds__(kBlock) k_gi_apply(DevScene S, NodeCols rec, i
 // per-launch lines, node sites, beam sites; the tile kernel's beam sites at 1024 + 6144 + 2048
 constexpr size_t kJitStatWords = 16384;
 
+// Page-locked host memory for the counts the host reads back to size its next launch (a pageable destination
+// costs ~16 us more per read-back: tools/microbench/sync.hip, profiles/r05_sync_latency.txt)
+template <typename T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    bool resize(size_t m) {  // (contents zeroed)
+        if (m > n) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            n = 0;
+            if (hipHostMalloc((void**)&p, m * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+                p = nullptr;
+                return false;
+            }
+            n = m;
+        }
+        std::memset(p, 0, n * sizeof(T));
+        return true;
+    }
+    T* data() { return p; }
+    const T* data() const { return p; }
+    size_t size() const { return n; }
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+};
+
 struct frt_scene_handle {
     int device = 0;
     frt::DevScene S{};
@@ -1674,7 +1707,10 @@ struct frt_scene_handle {
     uint32_t* mixed = nullptr;         // mixed (node, light) pairs, kMixSegs segments
     int64_t mixed_cap = 0;
     unsigned* mcount = nullptr;        // the segments' counters (kMixSegs lines of kMixLine words)
-    std::vector<unsigned> host_mcount;
+    uint64_t sync_epoch = 0;           // stream_sync calls (the level loop's early counter read-back)
+    PinnedBuf<unsigned> host_mcount;
+    PinnedBuf<unsigned long long> host_counters;  // (the level's queue counters, read back per level)
+    PinnedBuf<unsigned> host_lcount;  // (k_shade's list counts: the row sort's size, the lit-node statistic)
     int64_t* redo = nullptr;           // lanes handed back to the generic walk
     unsigned* redo_count = nullptr;
     unsigned redo_cap = 0;
@@ -1802,6 +1838,8 @@ static int grow(T** p, int64_t& cap, int64_t need) {
     cap = nc;
     return 0;
 }
+
+__global__ void k_warm(unsigned* p) { p[threadIdx.x] += 1u; }
 
 extern "C" {
 
@@ -2414,8 +2452,22 @@ int frt_device_warmup(int device) {
         return -1;
     }
     hip_ignore(hipFree(nullptr));  // (creates the context)
+    // the first allocation, copies both ways and kernel launch of a process set up the runtime's memory pools,
+    // staging buffers and this library's code object on the device: paid here, beside the caller's work
     void* p = nullptr;
-    if (hipMalloc(&p, 1 << 20) == hipSuccess) hip_ignore(hipFree(p));
+    if (hipMalloc(&p, 1 << 20) == hipSuccess) {
+        hipStream_t s = nullptr;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+            unsigned host[64] = {0};
+            hip_ignore(hipMemcpyAsync(p, host, sizeof(host), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_warm, dim3(1), dim3(64), 0, s, (unsigned*)p);
+            hip_ignore(hipMemcpyAsync(host, p, sizeof(host), hipMemcpyDeviceToHost, s));
+            hip_ignore(hipStreamSynchronize(s));
+            hip_ignore(hipStreamDestroy(s));
+        }
+        hip_ignore(hipFree(p));
+    }
+    (void)hipGetLastError();
     return 0;
 }
 
@@ -2654,7 +2706,10 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                     return fail("frt_scene_upload: light box / pair list allocation failed");
                 }
                 h->owned.push_back(h->mcount);
-                h->host_mcount.assign((size_t)frt::jit::kMixSegs * frt::jit::kMixLine, 0u);
+                if (!h->host_mcount.resize((size_t)frt::jit::kMixSegs * frt::jit::kMixLine)) {
+                    frt_scene_release(h);
+                    return fail("frt_scene_upload: pinned host buffer allocation failed");
+                }
                 if (std::getenv("FRT_JIT_STATS")) {
                     if (hipMalloc((void**)&h->jit_stats, kJitStatWords * sizeof(unsigned long long)) != hipSuccess) {
                         frt_scene_release(h);
@@ -2907,6 +2962,14 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
 
 static inline unsigned grid_for(int64_t n, int block = frt::kBlock) { return (unsigned)((n + block - 1) / block); }
 
+// a stream synchronize the level loop counts: the level's queue counters, copied to the host right after k_prepare,
+// are complete once any later synchronize returned (the level's own end-of-level synchronize is then skipped)
+static hipError_t stream_sync(frt_scene_handle* h) {
+    const hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) h->sync_epoch++;
+    return e;
+}
+
 // shading in two kernels (k_shade lists the nodes with light-point work, k_shade_lit shades them);
 // FRT_SHADE_SPLIT=0: one kernel for every node (A/B runs)
 static bool shade_split() {
@@ -3048,7 +3111,7 @@ static void launch_shadow_redo_f(frt_scene_handle* h, const frt::Batch& B, const
 
 // the block table of a segmented list (jit::SegTable) whose entries take lpe lanes each: returns the blocks,
 // `total` the entries (a segment past its capacity keeps its capacity: the error flag is set)
-static uint64_t seg_table(const std::vector<unsigned>& host_mcount, uint32_t segcap, uint64_t lpe,
+static uint64_t seg_table(const PinnedBuf<unsigned>& host_mcount, uint32_t segcap, uint64_t lpe,
                           frt::jit::SegTable& seg, uint64_t& total) {
     uint64_t nblk = 0;
     total = 0;
@@ -3084,7 +3147,16 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         const long long mp = mp_env ? std::atoll(mp_env) : 0;
         int64_t kMaxPairs = mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : (int64_t)((1ll << 31) - 1);
         // (the sub-part pass after the tile kernel: the per-ray kernel's list holds (node pair) * sub + q in 32 bits)
-        const bool tiled = h->jit_beam_on && h->tile > 0 && h->jit_tile && h->jit_list && h->tbox;
+        // Small levels (the deep bounces: a few thousand nodes) skip the beam stages: each stage's launch is sized
+        // on the host from the previous one's counts, a round trip (~15 us plus the idle GPU) that costs more than
+        // walking their rays one by one; the per-ray walk of every pair gives the same counts (FRT_JIT_MIN_PAIRS,
+        // default 2^18 (node, part) pairs)
+        static const int64_t min_pairs = [] {
+            const char* e = std::getenv("FRT_JIT_MIN_PAIRS");
+            return e ? (int64_t)std::atoll(e) : (int64_t)1 << 18;
+        }();
+        const bool beam_on = h->jit_beam_on && n * NP >= min_pairs;
+        const bool tiled = beam_on && h->tile > 0 && h->jit_tile && h->jit_list && h->tbox;
         const bool subbed = tiled && h->jit_sub && h->sub > 0 && h->light_psamp2 && h->light_sbox;
         if (subbed) kMaxPairs = std::min<int64_t>(kMaxPairs, (int64_t)(0xFFFFFFFFull / (uint64_t)h->sub));
         if (n * NP > kMaxPairs) {
@@ -3100,7 +3172,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         uint64_t total_mixed = 0;
         const uint32_t* direct_in = nullptr;  // (the sub / sub-tile list walked by the per-ray kernel directly)
         uint32_t direct_subq = 0, direct_nodes = 0;
-        if (h->jit_beam_on) {
+        if (beam_on) {
             frt::jit::SegTable tseg{};
             uint32_t tsegcap = 0;
             uint64_t list_blocks = 0, listed = 0;
@@ -3144,7 +3216,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 }
                 if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
                                    hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-                    hipStreamSynchronize(h->stream) != hipSuccess)
+                    stream_sync(h) != hipSuccess)
                     return;
                 list_blocks = seg_table(h->host_mcount, tsegcap, subbed ? (uint64_t)h->sub : (uint64_t)h->tile, tseg, listed);
                 h->tile_pairs += ntp;
@@ -3192,7 +3264,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     }
                     if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
                                        hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-                        hipStreamSynchronize(h->stream) != hipSuccess)
+                        stream_sync(h) != hipSuccess)
                         return;
                     uint64_t listed_s = 0;
                     const bool subtiled = h->jit_subtile && h->subtile > 0 && h->subtile < h->tile && h->stbox;
@@ -3247,7 +3319,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         }
                         if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
                                            hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-                            hipStreamSynchronize(h->stream) != hipSuccess)
+                            stream_sync(h) != hipSuccess)
                             return;
                         uint64_t listed_u = 0;
                         list_blocks = seg_table(h->host_mcount, s2segcap, (uint64_t)h->subtile, tseg, listed_u);
@@ -3332,7 +3404,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
             }
             if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
                                hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-                hipStreamSynchronize(h->stream) != hipSuccess)
+                stream_sync(h) != hipSuccess)
                 return;
             for (int j = 0; j < kMixSegs; ++j) total_mixed += std::min<uint64_t>(h->host_mcount[(size_t)j * kMixLine], segcap);
             h->node_mixed += total_mixed;
@@ -3347,7 +3419,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
             }
             total_mixed = (uint64_t)npairs;  // every pair, in order (frt_jit_shadow's all_pairs)
         }
-        uint32_t all_pairs = h->jit_beam_on ? 0u : 1u;
+        uint32_t all_pairs = beam_on ? 0u : 1u;
         // lanes per pair (a part of frt_jit_part_size() samples, or a sub-part's slot after frt_jit_sub);
         // tid / lpp by multiply-shift
         uint32_t subq = direct_in ? direct_subq : subbed ? 1u : 0u;
@@ -4134,7 +4206,10 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->photons[0] = h->gi.photons[0];
         st->photons[1] = h->gi.photons[1];
     }
-    std::vector<unsigned long long> host_counters((size_t)kQueueSegs * kCounterLine);
+    if (!h->host_counters.resize((size_t)kQueueSegs * kCounterLine) ||
+        !h->host_lcount.resize((size_t)kShadeSegs * jit::kMixLine))
+        return fail("render: pinned host buffer allocation failed");
+    auto& host_counters = h->host_counters;
     for (int64_t p0 = 0; p0 < npix; p0 += pix_per_batch) {
         const int64_t bp = std::min<int64_t>(pix_per_batch, npix - p0);
         const int64_t ns = bp * spp;
@@ -4202,6 +4277,11 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                                    subtiles ? h->stbox : nullptr, stl);
                 FRT_HIP(hipGetLastError());
             }
+            // the next level's queue counts are final here (k_prepare appends the level's rays): their copy rides on
+            // the shadow pass's first synchronize, and the level ends without one of its own
+            FRT_HIP(hipMemcpyAsync(host_counters.data(), h->counters, host_counters.size() * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, h->stream));
+            const uint64_t counters_epoch = h->sync_epoch;
             if (h->S.cfg.include_direct && h->samples_per_node > 0) {
                 KTimer t(h, st, 1);
                 launch_shadow(h, B, L.head, n, L.counts);
@@ -4255,10 +4335,10 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                     hipLaunchKernelGGL(k_lit_rows, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.head,
                                        h->shade_lit, h->shade_lcount, segcap, h->sort_light, keys, vals);
                     // (the listed count on the host: the sort's size)
-                    std::vector<unsigned> lc((size_t)kShadeSegs * jit::kMixLine);
+                    auto& lc = h->host_lcount;
                     FRT_HIP(hipMemcpyAsync(lc.data(), h->shade_lcount, lc.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
                                            h->stream));
-                    FRT_HIP(hipStreamSynchronize(h->stream));
+                    FRT_HIP(stream_sync(h));
                     int64_t listed = 0;
                     for (int sgi = 0; sgi < kShadeSegs; ++sgi) listed += lc[(size_t)sgi * jit::kMixLine];
                     if (st != nullptr) st->lit_nodes += (uint64_t)listed;
@@ -4272,7 +4352,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                     }
                 }
                 if (split && st != nullptr && !sorted) {  // (the stats frame: the listed count, frt_frame_stats.lit_nodes)
-                    std::vector<unsigned> lc((size_t)kShadeSegs * jit::kMixLine);
+                    auto& lc = h->host_lcount;
                     FRT_HIP(hipMemcpyAsync(lc.data(), h->shade_lcount, lc.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
                                            h->stream));
                     FRT_HIP(hipStreamSynchronize(h->stream));
@@ -4290,9 +4370,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 KTimer t(h, st, 7);
                 if (shade_gi(h, B, L, n, st)) return -1;
             }
-            FRT_HIP(hipMemcpyAsync(host_counters.data(), h->counters, host_counters.size() * sizeof(unsigned long long),
-                                   hipMemcpyDeviceToHost, h->stream));
-            FRT_HIP(hipStreamSynchronize(h->stream));
+            if (h->sync_epoch == counters_epoch) FRT_HIP(stream_sync(h));  // (no synchronize since the counters' copy)
             // the next level's queue segments: prefix counts (a segment past its capacity is an error)
             int64_t next = 0;
             bool overflow = false;

@@ -190,6 +190,8 @@ now_ms(void)
 /* one device's share of the frame: upload, render rows k, k+N, k+2N, ..., release */
 typedef struct {
     const frt_scene *fs;
+    frt_scene_handle *h;      /* in: a kept handle of the same scene and device (NULL: upload); out: the handle */
+    int keep;                 /* keep the handle for the next render_multi instead of releasing it */
     int device, k, n;
     int64_t height, width;
     uint64_t seed;
@@ -205,14 +207,16 @@ static void *
 device_worker(void *arg)
 {
     device_job *j = (device_job *)arg;
-    frt_scene_handle *h = NULL;
+    frt_scene_handle *h = j->h;
     const double t0 = now_ms();
-    j->rc = frt_scene_upload(j->fs, j->device, &h);
-    j->upload_ms = now_ms() - t0;
-    frt_upload_phases(j->upload_phases, 8);
-    if (j->rc) {
-        snprintf(j->err, sizeof(j->err), "device %d: upload: %s", j->device, frt_last_error());
-        return NULL;
+    if (h == NULL) {
+        j->rc = frt_scene_upload(j->fs, j->device, &h);
+        j->upload_ms = now_ms() - t0;
+        frt_upload_phases(j->upload_phases, 8);
+        if (j->rc) {
+            snprintf(j->err, sizeof(j->err), "device %d: upload: %s", j->device, frt_last_error());
+            return NULL;
+        }
     }
     const double t1 = now_ms();
     frt_frame_params p;
@@ -227,9 +231,73 @@ device_worker(void *arg)
         snprintf(j->err, sizeof(j->err), "device %d: render: %s", j->device, frt_last_error());
     }
     const double t2 = now_ms();
-    frt_scene_release(h);
+    if (j->keep) {
+        j->h = h;  /* (render_multi keeps it, or releases it once when the call fails) */
+    } else {
+        frt_scene_release(h);
+        j->h = NULL;
+    }
     j->release_ms = now_ms() - t2;
     return NULL;
+}
+
+/*
+ * The handles of the last render_multi stay alive (FRT_RM_KEEP=0: released at once, as before): a later call
+ * with the same flattened scene on the same devices renders on them without uploading the scene, compiling or
+ * loading its kernels or allocating the level state again, and the one call a generated main() makes does not
+ * wait for the release (the process's exit frees the device memory, as it frees the reference's per-thread
+ * world copies). A call with another scene or device list releases them first.
+ */
+static struct {
+    int n;
+    int dev[64];
+    frt_scene_handle *h[64];
+    frt_scene fs;  /* the flattened scene they were uploaded from (owned) */
+} g_kept;
+
+static int
+same_bytes(const void *a, const void *b, size_t n)
+{
+    return n == 0 || (a != NULL && b != NULL && memcmp(a, b, n) == 0);
+}
+
+/* the same flattened scene, byte for byte (padding included: a difference there only costs a fresh upload) */
+static int
+scenes_equal(const frt_scene *a, const frt_scene *b)
+{
+    if (a->num_nodes != b->num_nodes || a->num_roots != b->num_roots || a->num_xforms != b->num_xforms ||
+        a->prim_len != b->prim_len || a->num_materials != b->num_materials || a->num_patterns != b->num_patterns ||
+        a->num_textures != b->num_textures || a->texel_len != b->texel_len || a->num_lights != b->num_lights ||
+        a->light_point_len != b->light_point_len || memcmp(&a->camera, &b->camera, sizeof(a->camera)) != 0 ||
+        memcmp(&a->config, &b->config, sizeof(a->config)) != 0) {
+        return 0;
+    }
+    const size_t nst = 2 * (size_t)a->camera.usteps * (size_t)a->camera.vsteps;
+    return same_bytes(a->nodes, b->nodes, sizeof(frt_node) * (size_t)a->num_nodes) &&
+           same_bytes(a->roots, b->roots, sizeof(int32_t) * (size_t)a->num_roots) &&
+           same_bytes(a->xforms, b->xforms, sizeof(double) * 16 * (size_t)a->num_xforms) &&
+           same_bytes(a->prim_data, b->prim_data, sizeof(double) * (size_t)a->prim_len) &&
+           same_bytes(a->materials, b->materials, sizeof(frt_material) * (size_t)a->num_materials) &&
+           same_bytes(a->patterns, b->patterns, sizeof(frt_pattern) * (size_t)a->num_patterns) &&
+           same_bytes(a->textures, b->textures, sizeof(frt_texture) * (size_t)a->num_textures) &&
+           same_bytes(a->texels, b->texels, sizeof(double) * (size_t)a->texel_len) &&
+           same_bytes(a->lights, b->lights, sizeof(frt_light) * (size_t)a->num_lights) &&
+           same_bytes(a->light_points, b->light_points, sizeof(double) * (size_t)a->light_point_len) &&
+           same_bytes(a->sample_table, b->sample_table, sizeof(double) * nst);
+}
+
+static void
+release_kept(void)
+{
+    for (int k = 0; k < g_kept.n; ++k) {
+        if (g_kept.h[k] != NULL) {
+            frt_scene_release(g_kept.h[k]);
+        }
+    }
+    if (g_kept.n > 0) {
+        frt_flat_scene_free(&g_kept.fs);
+    }
+    g_kept.n = 0;
 }
 
 /* the phases of the last render_multi on this process, in ms (frt_render_multi_phases) */
@@ -239,8 +307,8 @@ static double g_rm_phases[16];
  * Diagnostics: the phases of the last render_multi, in ms: out[0] flatten, [1] upload (the slowest device),
  * [2..9] that device's frt_upload_phases, [10] render of its rows incl. the copy to host memory (the slowest
  * device), [11] placing the rows into the canvas, [12] release, [13] total, [14] the devices' runtime
- * initialisation (frt_device_warmup, on threads beside the flatten), [15] the wait for it after the flatten.
- * Writes min(n, 16); returns 16.
+ * initialisation (frt_device_warmup, on threads beside the flatten, once per device and process), [15] the wait
+ * for it after the flatten. Writes min(n, 16); returns 16.
  */
 int
 frt_render_multi_phases(double *out, int n)
@@ -256,6 +324,8 @@ typedef struct {
     double ms;
 } warmup_job;
 
+static int g_warmed[64];  /* devices frt_device_warmup ran on in this process (render_multi's thread only) */
+
 static void *
 warmup_worker(void *arg)
 {
@@ -265,6 +335,7 @@ warmup_worker(void *arg)
     j->ms = now_ms() - t0;
     return NULL;
 }
+
 
 /*
  * The drop-in entry point (reference renderer.c:244-281). Rows are interleaved
@@ -300,12 +371,15 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     pthread_t wt[FRT_MAX_RENDER_DEVICES];
     int nw = 0;
     for (int k = 0; k < n; ++k) {
-        int seen = 0;
+        int seen = dev[k] < 64 && g_warmed[dev[k]];  /* (once per device and process) */
         for (int q = 0; q < nw; ++q) {
             seen = seen || wj[q].device == dev[k];
         }
         if (seen) {
             continue;
+        }
+        if (dev[k] < 64) {
+            g_warmed[dev[k]] = 1;
         }
         wj[nw].device = dev[k];
         wj[nw].ms = 0.0;
@@ -328,6 +402,16 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
         memset(c->arr, 0, width * height * sizeof(Color));
         return c;
     }
+    const char *keep_env = getenv("FRT_RM_KEEP");
+    const int keep = !(keep_env != NULL && atoi(keep_env) == 0) && n <= 64;
+    int reuse = keep && g_kept.n == n;
+    for (int k = 0; reuse && k < n; ++k) {
+        reuse = g_kept.dev[k] == dev[k] && g_kept.h[k] != NULL;
+    }
+    reuse = reuse && scenes_equal(&fs, &g_kept.fs);
+    if (!reuse) {
+        release_kept();
+    }
     const char *seed_env = getenv("FRT_SEED");
     const uint64_t seed = seed_env ? strtoull(seed_env, NULL, 10) : 0x5eedULL;
     const char *stats_path = getenv("FRT_STATS_OUT");
@@ -338,6 +422,8 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
         device_job *j = &jobs[k];
         const int64_t nrows = ((int64_t)height - k + n - 1) / n;
         j->fs = &fs;
+        j->h = reuse ? g_kept.h[k] : NULL;
+        j->keep = keep;
         j->device = dev[k];
         j->k = k;
         j->n = n;
@@ -420,6 +506,32 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     }
     for (int k = 0; jobs != NULL && n > 1 && k < n; ++k) {
         free(jobs[k].rows);
+    }
+    int kept_all = keep && !failed && jobs != NULL;
+    for (int k = 0; kept_all && k < n; ++k) {
+        kept_all = jobs[k].h != NULL;
+    }
+    if (kept_all) {
+        if (!reuse) {  /* (the new scene's handles and flattened scene) */
+            g_kept.n = n;
+            for (int k = 0; k < n; ++k) {
+                g_kept.dev[k] = dev[k];
+                g_kept.h[k] = jobs[k].h;
+            }
+            g_kept.fs = fs;
+            memset(&fs, 0, sizeof(fs));
+        }
+    } else {
+        /* (a failed call keeps nothing: every job's handle, a reused one included, released once) */
+        for (int k = 0; jobs != NULL && k < n; ++k) {
+            if (jobs[k].h != NULL) {
+                frt_scene_release(jobs[k].h);
+            }
+        }
+        if (reuse) {
+            frt_flat_scene_free(&g_kept.fs);
+            g_kept.n = 0;
+        }
     }
     free(jobs);
     free(th);

@@ -11,6 +11,11 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 if ORACLE_DIR not in sys.path:
     sys.path.insert(0, ORACLE_DIR)
 
+# The test scenes are small: every level of them would skip the shadow pass's beam stages (frt_engine.hip
+# launch_shadow: levels under FRT_JIT_MIN_PAIRS (node, light part) pairs walk their rays one by one). The tests
+# exercise the stages at every size; test_jit.py::test_small_levels_skip_beam_stages_bit_identical checks the default.
+os.environ.setdefault("FRT_JIT_MIN_PAIRS", "0")
+
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 ASSETS = os.path.join(GOLDEN, "assets")
 

@@ -190,8 +190,9 @@ def test_render_multi_shares_photon_maps_across_devices(built):
         return int(out[0]), int(out[1])
 
     sc = load_scene("cornell_gi_24")
-    saved = {k: os.environ.get(k) for k in ("FRT_SHARE_PHOTONS", "FRT_SEED")}
+    saved = {k: os.environ.get(k) for k in ("FRT_SHARE_PHOTONS", "FRT_SEED", "FRT_RM_KEEP")}
     os.environ["FRT_SEED"] = "424242"  # (a seed no other test renders this scene with: no maps kept from before)
+    os.environ["FRT_RM_KEEP"] = "0"  # (every call uploads: a kept handle would reuse its maps)
     try:
         os.environ["FRT_SHARE_PHOTONS"] = "0"
         t0, s0 = passes()
@@ -413,3 +414,32 @@ def test_row_sorted_shading_equals_list_order(built, name, rows):
     plain = _render_env(name, {"FRT_SHADE_SORT": "0"}, **kw)
     assert np.isfinite(sorted_).all() and sorted_[:, :, :3].max() > 0
     assert np.array_equal(sorted_, plain)
+
+
+def test_render_multi_keeps_handles_between_calls(built):
+    """render_multi keeps the last call's device handles (host/frt_render.c g_kept): a call with the same flattened
+    scene and devices renders on them without an upload; another scene or device list releases them first. The
+    canvases equal fresh uploads bit for bit (FRT_RM_KEEP=0), through a sequence that switches scenes and device
+    lists, and the reuse shows in the phases (no upload time on a repeated call)."""
+    from fast_ray_tracer_amd.runtime import render_multi, render_multi_phases
+    a, b = load_scene("cornell_direct_64_4x4"), load_scene("checkered_sphere_200")
+    saved = os.environ.get("FRT_RM_KEEP")
+    try:
+        os.environ["FRT_RM_KEEP"] = "0"
+        ref_a, ref_b = render_multi(a, devices="0"), render_multi(b, devices="0")
+        ref_a2 = render_multi(a, devices="0,0")
+        os.environ["FRT_RM_KEEP"] = "1"
+        outs = []
+        for sc, devs in ((a, "0"), (a, "0"), (b, "0"), (b, "0"), (a, "0,0"), (a, "0,0"), (a, "0")):
+            outs.append(render_multi(sc, devices=devs))
+            if len(outs) in (2, 4, 6):  # (a repeat of the previous call: the kept handles, no upload)
+                assert render_multi_phases()["upload"] == 0.0, render_multi_phases()
+            if len(outs) in (1, 3, 5, 7):
+                assert render_multi_phases()["upload"] > 0.0, render_multi_phases()
+    finally:
+        if saved is None:
+            os.environ.pop("FRT_RM_KEEP", None)
+        else:
+            os.environ["FRT_RM_KEEP"] = saved
+    for got, ref in zip(outs, (ref_a, ref_a, ref_b, ref_b, ref_a2, ref_a2, ref_a)):
+        assert np.array_equal(got, ref)

@@ -198,3 +198,17 @@ def test_tile_kernels_on_shipped_multi_row_light(built, tmp_path):
         img0, st0 = _render_env_process("cornell_shipped_1920x1080_8x8", {"FRT_JIT_TILE": "0"}, tmp_path / "n.npy", **kw)
         assert st0[0] == 1 and st0[1] == 0, st0
         assert np.array_equal(img0, ref), rows
+
+
+@pytest.mark.gpu
+def test_small_levels_skip_beam_stages_bit_identical(built, tmp_path):
+    """Levels with fewer than FRT_JIT_MIN_PAIRS (node, light part) pairs (default 2^18: the deep bounces) walk every
+    shadow ray one by one instead of taking the beam stages, whose launches are sized on the host (a round trip
+    each). The production default against the stages at every size (FRT_JIT_MIN_PAIRS=0, the test session's
+    setting): a band of the headline frame and two small scenes, bit for bit."""
+    for name, kw in (("cornell_direct_1920x1080_8x8", {"row_begin": 400, "row_end": 408}),
+                     ("reflect_refract_test_150", {}), ("cornell_direct_64_4x4", {})):
+        stages, st0 = _render_env_process(name, {"FRT_JIT_MIN_PAIRS": "0"}, tmp_path / "a.npy", **kw)
+        default, st1 = _render_env_process(name, {"FRT_JIT_MIN_PAIRS": str(1 << 18)}, tmp_path / "b.npy", **kw)
+        assert st0[0] == 1 and st1[0] == 1 and st0[1] > 0
+        assert np.array_equal(stages, default), name
