@@ -206,7 +206,9 @@ def issue_block(t: dict, avg_ms: float, units_per_launch: float, unit_name: str)
 
 def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> dict:
     """The per-ray shadow kernel (frt_jit_shadow; the generic k_shadow when the scene is not eligible),
-    timed by HIP events around its own launches (frt_frame_stats.sub_ms).
+    timed by HIP events around its own launches (frt_frame_stats.sub_ms). Algorithmic bytes (engine-side
+    shadow_kernel_bytes): per list entry its 8 bytes, per node of an entry its 40-byte ShadowHead once (not per ray:
+    the node's rays share it) and one 4-byte count, per ray of a multi-row light its 24-byte point.
 
     bound: "valu-issue" — the kernel moves few bytes (achieved / peak / frac below are its algorithmic
     HBM bytes against the 8 TB/s peak, as the bench contract asks) and is limited by instruction issue on
@@ -302,7 +304,9 @@ def frame_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> d
         flops = 64.0 * (f64[0] + f64[1] + f64[3]) + 128.0 * f64[2]
         ach = flops / (avg * 1e-3) / 1e12
         roof.update({"bound": "valu-fp64", "achieved": round(ach, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(ach / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_launch": round(flops)})
+                     "frac": round(ach / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_launch": round(flops),
+                     "fp64_flops_note": "64 x the wave instruction counts of the PMC pass (128 x for FMA): lanes a wave "
+                                        "masks off are counted as working, so the true FLOP rate is at most this"})
     elif pname.startswith("frt_jit"):
         roof.update({"bound": "valu-issue", "achieved": None, "peak": None, "unit": None, "frac": None,
                      "note": "instruction-issue bound; see roofline_shadow_pass.issue for the VALU / SALU fractions"})

@@ -1716,7 +1716,8 @@ struct frt_scene_handle {
     unsigned redo_cap = 0;
     frt_frame_stats* cur_st = nullptr;  // the instrumented frame's stats (sub-kernel timers), else null
     uint64_t rays_walked = 0;           // shadow rays walked one by one in this frame
-    uint64_t pairs_walked = 0;          // (node, light part) pairs they belong to
+    uint64_t pairs_walked = 0;          // (node, light part) pairs they belong to (list entries walked)
+    uint64_t heads_walked = 0;          // ShadowHeads the per-ray kernel read (a node per lane group of an entry)
     unsigned long long uniform_stats[3] = {0, 0, 0};  // FRT_JIT_STATS: (node, light) pairs all lit / all shadowed / mixed
     // k_shade's list of nodes with light-point work (kShadeSegs segments) and its segment counters
     uint32_t* shade_lit = nullptr;
@@ -3433,6 +3434,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
         h->rays_walked += total_mixed * lpp;  // (parts of fewer samples count their padding lanes too)
         h->pairs_walked += total_mixed;
+        h->heads_walked += direct_in ? total_mixed * direct_nodes : total_mixed;  // (ShadowHeads read: a node per lane group)
         KTimer tr(h, h->cur_st, 9);
         // the mixed pairs' blocks by segment (jit::SegTable); every pair in order without the pair kernel
         frt::jit::SegTable seg{};
@@ -4046,7 +4048,14 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
     const int64_t rays_per = (int64_t)cfg.gi_usteps * (int64_t)cfg.gi_vsteps;
     const bool gather = cfg.include_final_gather && rays_per > 0;
     if (gather) {
-        const int64_t kChunkRays = (int64_t)1 << 22;
+        // gather rays per chunk (FRT_GATHER_CHUNK): each chunk's estimate launch ends in a tail of its slowest queries;
+        // 2^22 / 2^24 / 2^25 rays gave 29.33 / 28.97 / 28.92 s GI frames (profiles/r05_ab_gi_chunk.txt); 2^24 keeps
+        // the chunk's buffers at 3.2 GB
+        static const int64_t kChunkRays = [] {
+            const char* e = std::getenv("FRT_GATHER_CHUNK");
+            const long long v = e ? std::atoll(e) : 0;
+            return v >= 1024 ? (int64_t)v : (int64_t)1 << 24;
+        }();
         const int64_t chunk = std::max<int64_t>(1, kChunkRays / rays_per);
         for (int64_t n0 = 0; n0 < n; n0 += chunk) {
             const int64_t m = std::min(chunk, n - n0);
@@ -4146,6 +4155,7 @@ static int render_impl(frt_scene_handle* h, const frt_frame_params* P, double* d
     h->cur_st = st;
     h->rays_walked = 0;
     h->pairs_walked = 0;
+    h->heads_walked = 0;
     h->tile_pairs = h->tile_mixed = h->node_pairs = h->node_mixed = h->sub_pairs = h->sub_mixed = 0;
     h->subtile_pairs = h->subtile_mixed = 0;
     const int rc = render_frame(h, P, dev_out, st);
@@ -4447,12 +4457,17 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->pruned_secondary = pruned;
         st->hits = hits;
         st->shadow_rays = h->S.cfg.include_direct ? hits * (uint64_t)h->samples_per_node : 0;
-        // DESIGN.md byte model of the per-ray shadow kernel: per walked (node, light part) pair its 4-byte list
-        // entry and 4-byte resume word and the node's ShadowHead read, one 4-byte count written; the generic
-        // walk: per shaded node the ShadowHead + one 4-byte count per light
+        // DESIGN.md byte model of the per-ray shadow kernel: per list entry its 4-byte entry and 4-byte resume word;
+        // per node of an entry its ShadowHead, read once for the entry's rays (heads_walked: an entry of the sub-part
+        // list holds a tile's 64 nodes, of the node-pair list one), and one 4-byte count added; with a multi-row light
+        // each ray's 24-byte point from its node's row (a single-row light's points stay in cache); the generic walk:
+        // per shaded node the ShadowHead + one 4-byte count per light
         constexpr double kHead = (double)sizeof(frt::ShadowHead);
+        bool multi = false;
+        for (const auto& L : h->host_lights) multi = multi || L.rows > 1;
         st->shadow_kernel_bytes = !(h->S.cfg.include_direct && h->samples_per_node > 0) ? 0.0
-                                  : h->jit_shadow != nullptr ? (double)h->pairs_walked * (4.0 + 4.0 + kHead + 4.0)
+                                  : h->jit_shadow != nullptr ? (double)h->pairs_walked * 8.0 + (double)h->heads_walked * (kHead + 4.0) +
+                                                                   (multi ? 24.0 * (double)h->rays_walked : 0.0)
                                                              : (double)hits * (kHead + 4.0 * h->S.num_lights);
         st->errors = err;
         st->shadow_jit = h->jit_shadow != nullptr ? 1 : 0;
