@@ -1488,9 +1488,9 @@ constexpr int kGatherWavesPerBlock = FRT_GATHER_WAVES_PER_BLOCK;
 #define FRT_GATHER_REQ_PER_WAVE 64
 #endif
 constexpr int kGatherReqPerWave = FRT_GATHER_REQ_PER_WAVE;
-// (Tried and measured slower on cornell_gi_480x270_8x8: requests radix-sorted by a Morton key of their point,
-// 1793 -> 1855 ms plus 20 ms of sorting, and with the blocks dealt to the XCDs in contiguous runs 2600 ms:
-// the dense regions then crowd onto one XCD. The estimate is bound by instruction issue, not by L2 misses.)
+// (Round 3 sorted the requests by a Morton key with one shared counter, 1793 -> 1855 ms, and dealt contiguous
+// block runs to the XCDs, 2600 ms: the dense regions then crowd onto one XCD. Round 5's per-XCD queues that steal
+// the other groups' leftovers keep the balance: below.)
 // work: nullptr — wave w takes requests [w kGatherReqPerWave, (w + 1) kGatherReqPerWave); else a queue
 // counter: resident waves take kGatherBatch requests at a time until none are left (the dense queries'
 // waves no longer set the launch's tail)
@@ -1498,9 +1498,48 @@ constexpr int kGatherReqPerWave = FRT_GATHER_REQ_PER_WAVE;
 #define FRT_GATHER_BATCH 16
 #endif
 constexpr int kGatherBatch = FRT_GATHER_BATCH;
+constexpr int kGatherGroups = 8;  // (the XCDs: blocks blockIdx % 8 share one)
+// The estimate reads ~20 KB of the photon map per query and its queries, in gather order, scatter over the room:
+// every byte came from beyond the XCD's L2 (FETCH_SIZE x 2 per query = the byte model, 6.4 TB/s of fabric reads,
+// profiles/r03_pmc_k_gather_est_*.json), and 3 waves per SIMD estimate as fast as 4 (profiles/r05_ab_gi_order.txt):
+// the fabric, not the latency chain, bounds it. k_gather_keys gives each request a 30-bit Morton key of its point in
+// the photon grid's box (requests without an estimate last), a radix sort orders the requests' indices by it (perm),
+// and k_gather_est deals the sorted order to the 8 groups of blocks that share an XCD (blockIdx % 8: its own
+// contiguous eighth, taken kGatherBatch at a time, then the other groups' leftovers), so the queries in flight on
+// one XCD are neighbours and share the photons in its L2. Results go to each request's own slot: the order changes
+// nothing in a query's arithmetic (test_gather_order_equals_request_order).
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits to every third of 30
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_gather_keys(DevScene S, const GatherReq* __restrict__ req, int64_t n,
+                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const PhotonMapDev& M = S.pmaps[1];
+    const GatherReq& r = req[t];
+    uint32_t key = 1u << 30;  // (no estimate: after every point)
+    if (r.want) {
+        uint32_t q[3];
+        for (int k = 0; k < 3; ++k) {
+            const double ext = (double)max(M.dims[k], 1) * M.cell;
+            const double f = (r.pt[k] - M.origin[k]) / ext * 1024.0;
+            q[k] = f >= 1023.0 ? 1023u : f > 0.0 ? (uint32_t)f : 0u;  // (NaN: 0)
+        }
+        key = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+    }
+    keys[t] = key;
+    idx[t] = (uint32_t)t;
+}
+
 __global__ void __launch_bounds__(64 * kGatherWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8)))
 k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col,
-             unsigned* __restrict__ work) {
+             unsigned* __restrict__ work, const uint32_t* __restrict__ perm) {
     FRT_EST_LDS_W(lds, kGatherEstCap, kGatherWavesPerBlock);
     auto query = [&](int64_t t) {
         const GatherReq& r = req[t];
@@ -1536,19 +1575,35 @@ k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* _
     const int per = queue ? kGatherBatch : kGatherReqPerWave;
     int64_t t0 = ((int64_t)blockIdx.x * kGatherWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) *
                  kGatherReqPerWave;
-    for (bool first = true;; first = false) {  // (every wave leaves once the counter passes n)
+    // (perm: the sorted order, dealt in kGatherGroups contiguous ranges, one counter each on its own line; a wave starts
+    // at its block's group and moves on to the next group when that range is done)
+    int g = perm != nullptr ? (int)(blockIdx.x % kGatherGroups) : 0;
+    int tried = 0;
+    int64_t lo = 0, len = n;
+    auto group_range = [&](int gg) {
+        lo = n * gg / kGatherGroups;
+        len = n * (gg + 1) / kGatherGroups - lo;
+    };
+    if (perm != nullptr) group_range(g);
+    for (bool first = true;; first = false) {  // (every wave leaves once every counter passes its range)
         if (queue) {
             unsigned base = 0;
-            if (est_lane() == 0) base = atomicAdd(work, (unsigned)kGatherBatch);
+            if (est_lane() == 0) base = atomicAdd(work + (perm != nullptr ? g * 64 : 0), (unsigned)kGatherBatch);
             t0 = (int64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)__shfl(base, 0, 64));
+            if (perm != nullptr && t0 >= len) {  // (this group's range is done: the next group's)
+                if (++tried >= kGatherGroups) break;
+                g = (g + 1) % kGatherGroups;
+                group_range(g);
+                continue;
+            }
         } else if (!first) {
             break;
         }
-        if (t0 >= n) break;
+        if (t0 >= (perm != nullptr ? len : n)) break;
         for (int j = 0; j < per; ++j) {
-            const int64_t t = t0 + j;
-            if (t >= n) break;
-            query(t);
+            const int64_t ts = t0 + j;
+            if (ts >= (perm != nullptr ? len : n)) break;
+            query(perm != nullptr ? (int64_t)perm[lo + ts] : ts);
         }
     }
 }
@@ -1789,7 +1844,9 @@ struct frt_scene_handle {
         double* gcol = nullptr;
         frt::GatherReq* greq = nullptr;
         int64_t gq_cap = 0, ghits_cap = 0, gcol_cap = 0, greq_cap = 0;
-        unsigned* gwork = nullptr;  // k_gather_est's queue counter
+        unsigned* gwork = nullptr;  // k_gather_est's queue counters (one 256-byte line per XCD group)
+        uint32_t* gkeys = nullptr;  // the requests' sort keys and indices (and the sort's alternate buffers)
+        int64_t gkeys_cap = 0;
         double* extra = nullptr;
         double* fgather = nullptr;
         int64_t extra_cap = 0, fgather_cap = 0;
@@ -2900,6 +2957,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(G.gcol));
         hip_ignore(hipFree(G.greq));
         hip_ignore(hipFree(G.gwork));
+        hip_ignore(hipFree(G.gkeys));
         hip_ignore(hipFree(G.extra));
         hip_ignore(hipFree(G.fgather));
     }
@@ -4079,19 +4137,36 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
                 const char* qenv = std::getenv("FRT_GATHER_QUEUE");
                 const bool queue = !(qenv && std::strcmp(qenv, "0") == 0) && rays < (int64_t)0xF0000000u;
                 if (queue) {
-                    if (!G.gwork) FRT_HIP(hipMalloc((void**)&G.gwork, sizeof(unsigned)));
-                    FRT_HIP(hipMemsetAsync(G.gwork, 0, sizeof(unsigned), h->stream));
+                    if (!G.gwork) FRT_HIP(hipMalloc((void**)&G.gwork, kGatherGroups * 64 * sizeof(unsigned)));
+                    FRT_HIP(hipMemsetAsync(G.gwork, 0, kGatherGroups * 64 * sizeof(unsigned), h->stream));
+                    // the requests in the spatial order of their points from 4096 of them (FRT_GATHER_SORT=0: gather
+                    // order, =1: sorted at any count)
+                    static const int sort_mode = std::getenv("FRT_GATHER_SORT") ? std::atoi(std::getenv("FRT_GATHER_SORT")) : -1;
+                    const uint32_t* perm = nullptr;
+                    if (sort_mode != 0 && (rays >= 4096 || sort_mode == 1) && rays < (int64_t)0x7FFFFFFF) {
+                        if (grow(&G.gkeys, G.gkeys_cap, 4 * rays)) return -1;
+                        uint32_t *k0 = G.gkeys, *k1 = G.gkeys + rays, *i0 = G.gkeys + 2 * rays, *i1 = G.gkeys + 3 * rays;
+                        hipLaunchKernelGGL(k_gather_keys, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, G.greq, rays,
+                                           k0, i0);
+                        size_t tmp_bytes = 0;
+                        FRT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, i0, i1, (int)rays, 0, 31,
+                                                                   h->stream));
+                        if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
+                        FRT_HIP(hipcub::DeviceRadixSort::SortPairs((void*)h->scan_tmp, tmp_bytes, k0, k1, i0, i1, (int)rays, 0,
+                                                                   31, h->stream));
+                        perm = i1;
+                    }
                     int cus = 0;
                     FRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
                     // every wave resident at once: FRT_EST_WAVES per SIMD, 4 SIMDs per CU
                     const int64_t blocks = std::max<int64_t>(1, (int64_t)cus * 4 * FRT_EST_WAVES / kGatherWavesPerBlock);
                     hipLaunchKernelGGL(k_gather_est, dim3((unsigned)blocks), dim3(64 * kGatherWavesPerBlock), 0, h->stream,
-                                       h->S, G.greq, rays, G.gcol, G.gwork);
+                                       h->S, G.greq, rays, G.gcol, G.gwork, perm);
                 } else {
                     const int64_t gwaves = (rays + kGatherReqPerWave - 1) / kGatherReqPerWave;
                     hipLaunchKernelGGL(k_gather_est, dim3((unsigned)((gwaves + kGatherWavesPerBlock - 1) / kGatherWavesPerBlock)),
                                        dim3(64 * kGatherWavesPerBlock), 0, h->stream, h->S, G.greq, rays, G.gcol,
-                                       (unsigned*)nullptr);
+                                       (unsigned*)nullptr, (const uint32_t*)nullptr);
                 }
             }
             hipLaunchKernelGGL(k_gather_reduce, dim3(grid_for(m)), dim3(kBlock), 0, h->stream, h->S, L.rec, n0, m, G.gcol,
