@@ -326,19 +326,24 @@ def frame_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> d
 def gather_roofline(gd: dict) -> dict:
     """k_gather_est (the GI frame's dominant kernel): the photon-map estimate per final-gather ray.
     Algorithmic bytes per query (profiles/r03_gi_estimate_counters.json: device counters of the estimate,
-    tools/prof_gi_full.sh): the binary32 positions of the candidates it scans (16 B each), the 80-byte
-    records of the photons it uses, its 96-byte request and 24-byte result. `achieved` = that per query x
-    this frame's queries per launch over the live event-timed launch duration; `traffic` = the PMC
-    FETCH_SIZE (x2, the guide's gfx950 correction for wide coalesced reads) + WRITE_SIZE per launch of
-    the same workload (profiles/r03_pmc_k_gather_est_cornell_gi_1920x1080_8x8.json)."""
+    tools/prof_gi_full.sh; the algorithm has not changed since): the binary32 positions of the candidates it
+    scans (16 B each), the 80-byte records of the photons it uses, its 96-byte request and 24-byte result.
+    `achieved` = that per query x this frame's queries per launch over the live event-timed launch duration;
+    `traffic` = the PMC FETCH_SIZE (x2, the guide's gfx950 correction for wide coalesced reads) + WRITE_SIZE per
+    launch of the same workload (the newest profiles/r*_pmc_k_gather_est_cornell_gi_1920x1080_8x8.json).
+
+    bound: "valu-issue" since round 5. The requests are estimated in the Morton order of their points, dealt to
+    per-XCD queues, so one XCD's queries share the photons in its L2 (TCC hit rate 37 % -> 96 %, FETCH_SIZE / 21,
+    profiles/r05_ab_gi_sort.txt): the ~20 KB a query reads are L2 hits, the byte rate below is an L2-request
+    rate (not HBM), and `issue` holds the VALU / SALU issue rates of the PMC pass over the live launch time."""
     n = gd["sub_launches"]["k_gather_est"]
     avg_ms = gd["sub_ms"]["k_gather_est"] / n
-    roof = {"bound": "latency", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+    roof = {"bound": "valu-issue", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
             "kernel": "k_gather_est", "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": n,
             "bytes_model": "L2-request bytes: the byte model counts every byte the estimate requests from the memory "
-                           "system (candidate positions, photon records, request, result); the ~100 MB photon map stays "
-                           "in L2 / Infinity Cache, so this is not HBM traffic and frac is not an HBM fraction. The "
-                           "kernel is bound by each query's chain of dependent round trips (wait_any_frac)"}
+                           "system (candidate positions, photon records, request, result); with the requests in "
+                           "spatial order they hit the XCDs' L2, so this is not HBM traffic and frac is not an HBM "
+                           "fraction (traffic is the HBM side)"}
     model = os.path.join(ROOT, "profiles", "r03_gi_estimate_counters.json")
     if os.path.exists(model):
         m = json.load(open(model))
@@ -355,13 +360,18 @@ def gather_roofline(gd: dict) -> dict:
     if found:
         path, t = found
         traffic = 2.0 * t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)
+        queries = gd["gather_rays"] / n
         roof.update({"traffic": round(traffic), "traffic_source": os.path.relpath(path, ROOT),
                      "rocprof_avg_launch_ms": round(t.get("rocprof_avg_ms", 0.0), 4),
                      # per query: the launch's counts over its queries (the estimate's waves take requests
                      # from a queue, so waves and queries are not in a fixed ratio)
-                     "valu_insts_per_query": round(t["SQ_INSTS_VALU_per_launch"] / (gd["gather_rays"] / n), 1),
-                     "salu_insts_per_query": round(t["SQ_INSTS_SALU_per_launch"] / (gd["gather_rays"] / n), 1),
-                     "wait_any_frac": round(t.get("sq_wait_any_frac_of_wave_cycles", 0.0), 3)})
+                     "valu_insts_per_query": round(t["SQ_INSTS_VALU_per_launch"] / queries, 1),
+                     "salu_insts_per_query": round(t["SQ_INSTS_SALU_per_launch"] / queries, 1),
+                     "wait_any_frac": round(t.get("sq_wait_any_frac_of_wave_cycles", 0.0), 3),
+                     "issue": issue_block(t, avg_ms, queries, "queries")})
+        if "TCC_HIT_sum_per_launch" in t and "TCC_MISS_sum_per_launch" in t:
+            hm = t["TCC_HIT_sum_per_launch"] + t["TCC_MISS_sum_per_launch"]
+            roof["l2_hit_rate"] = round(t["TCC_HIT_sum_per_launch"] / hm, 4) if hm else None
     return roof
 
 

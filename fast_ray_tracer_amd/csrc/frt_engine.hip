@@ -1408,12 +1408,36 @@ struct GatherReq {
     int32_t want, pad;
 };
 
+// the sort key of a gather request (k_gather_est's spatial order, below): a 21-bit Morton code of its point in the
+// photon grid's box, 128 cells per axis, and bit 21 set for requests without an estimate (last); the radix sort
+// then takes 3 passes of 8 bits
+constexpr int kGatherKeyBits = 22;
+__device__ __forceinline__ uint32_t spread7(uint32_t v) {  // 7 bits to every third of 21
+    v &= 0x7Fu;
+    v = (v | (v << 8)) & 0x0000F00Fu;
+    v = (v | (v << 4)) & 0x000C30C3u;
+    v = (v | (v << 2)) & 0x00249249u;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t gather_key(const PhotonMapDev& M, bool want, const double* pt) {
+    if (!want) return 1u << 21;
+    uint32_t q[3];
+    for (int k = 0; k < 3; ++k) {
+        const double ext = (double)max(M.dims[k], 1) * M.cell;
+        const double f = (pt[k] - M.origin[k]) / ext * 128.0;
+        q[k] = f >= 127.0 ? 127u : f > 0.0 ? (uint32_t)f : 0u;  // (NaN: 0)
+    }
+    return spread7(q[0]) | (spread7(q[1]) << 1) | (spread7(q[2]) << 2);
+}
+
 // color_at_gi + shade_hit_gi (renderer.c:320-345, 627-645) per gather ray up to the estimate: the
 // hit's prepare_computations and material, written as a GatherReq
 template <bool kPat>
 __global__ void __launch_bounds__(kBlock) k_gather_hit(DevScene S, uint64_t seed, const QueuedRay* __restrict__ gq,
                                                        const HitRec* __restrict__ hits, int64_t n,
-                                                       GatherReq* __restrict__ req) {
+                                                       GatherReq* __restrict__ req, uint32_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ idx) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     bool want = false;
@@ -1464,6 +1488,10 @@ __global__ void __launch_bounds__(kBlock) k_gather_hit(DevScene S, uint64_t seed
     r.want = want ? 1 : 0;
     r.pad = 0;
     req[t] = r;
+    if (keys) {  // (the estimate's spatial order)
+        keys[t] = gather_key(S.pmaps[1], want, pt);
+        idx[t] = (uint32_t)t;
+    }
 }
 
 // the gather hits' photon estimates (lighting_gi, renderer.c:863-892) in a kernel that holds only
@@ -1502,41 +1530,12 @@ constexpr int kGatherGroups = 8;  // (the XCDs: blocks blockIdx % 8 share one)
 // The estimate reads ~20 KB of the photon map per query and its queries, in gather order, scatter over the room:
 // every byte came from beyond the XCD's L2 (FETCH_SIZE x 2 per query = the byte model, 6.4 TB/s of fabric reads,
 // profiles/r03_pmc_k_gather_est_*.json), and 3 waves per SIMD estimate as fast as 4 (profiles/r05_ab_gi_order.txt):
-// the fabric, not the latency chain, bounds it. k_gather_keys gives each request a 30-bit Morton key of its point in
-// the photon grid's box (requests without an estimate last), a radix sort orders the requests' indices by it (perm),
+// the fabric, not the latency chain, bounds it. k_gather_hit gives each request a Morton key of its point in the
+// photon grid's box (gather_key; requests without an estimate last), a radix sort orders the requests' indices by it (perm),
 // and k_gather_est deals the sorted order to the 8 groups of blocks that share an XCD (blockIdx % 8: its own
 // contiguous eighth, taken kGatherBatch at a time, then the other groups' leftovers), so the queries in flight on
 // one XCD are neighbours and share the photons in its L2. Results go to each request's own slot: the order changes
 // nothing in a query's arithmetic (test_gather_order_equals_request_order).
-__device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits to every third of 30
-    v &= 0x3FFu;
-    v = (v | (v << 16)) & 0x030000FFu;
-    v = (v | (v << 8)) & 0x0300F00Fu;
-    v = (v | (v << 4)) & 0x030C30C3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-
-__global__ void __launch_bounds__(kBlock) k_gather_keys(DevScene S, const GatherReq* __restrict__ req, int64_t n,
-                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ idx) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const PhotonMapDev& M = S.pmaps[1];
-    const GatherReq& r = req[t];
-    uint32_t key = 1u << 30;  // (no estimate: after every point)
-    if (r.want) {
-        uint32_t q[3];
-        for (int k = 0; k < 3; ++k) {
-            const double ext = (double)max(M.dims[k], 1) * M.cell;
-            const double f = (r.pt[k] - M.origin[k]) / ext * 1024.0;
-            q[k] = f >= 1023.0 ? 1023u : f > 0.0 ? (uint32_t)f : 0u;  // (NaN: 0)
-        }
-        key = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
-    }
-    keys[t] = key;
-    idx[t] = (uint32_t)t;
-}
-
 __global__ void __launch_bounds__(64 * kGatherWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FRT_EST_WAVES, 8)))
 k_gather_est(DevScene S, const GatherReq* __restrict__ req, int64_t n, double* __restrict__ gather_col,
              unsigned* __restrict__ work, const uint32_t* __restrict__ perm) {
@@ -4126,34 +4125,34 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
             frt::Batch Bg = B;  // the gather rays form one contiguous queue
             Bg.qprefix = nullptr;
             launch_trace(h, Bg, G.gq, rays, G.ghits, 0);
+            // FRT_GATHER_QUEUE=0: the static request ranges (A/B runs)
+            const char* qenv = std::getenv("FRT_GATHER_QUEUE");
+            const bool queue = !(qenv && std::strcmp(qenv, "0") == 0) && rays < (int64_t)0xF0000000u;
+            // the requests in the spatial order of their points from 4096 of them (FRT_GATHER_SORT=0: gather order,
+            // =1: sorted at any count)
+            static const int sort_mode = std::getenv("FRT_GATHER_SORT") ? std::atoi(std::getenv("FRT_GATHER_SORT")) : -1;
+            const bool sorted = queue && sort_mode != 0 && (rays >= 4096 || sort_mode == 1) && rays < (int64_t)0x7FFFFFFF;
+            if (sorted && grow(&G.gkeys, G.gkeys_cap, 4 * rays)) return -1;
+            uint32_t *k0 = G.gkeys, *k1 = G.gkeys + rays, *i0 = G.gkeys + 2 * rays, *i1 = G.gkeys + 3 * rays;
             {
                 KTimer th(h, st, 11);
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_gather_hit<true> : k_gather_hit<false>, dim3(grid_for(rays)),
-                                   dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq, G.ghits, rays, G.greq);
+                                   dim3(kBlock), 0, h->stream, h->S, B.seed, G.gq, G.ghits, rays, G.greq,
+                                   sorted ? k0 : nullptr, sorted ? i0 : nullptr);
             }
             {
                 KTimer te(h, st, 10);
-                // FRT_GATHER_QUEUE=0: the static request ranges (A/B runs)
-                const char* qenv = std::getenv("FRT_GATHER_QUEUE");
-                const bool queue = !(qenv && std::strcmp(qenv, "0") == 0) && rays < (int64_t)0xF0000000u;
                 if (queue) {
                     if (!G.gwork) FRT_HIP(hipMalloc((void**)&G.gwork, kGatherGroups * 64 * sizeof(unsigned)));
                     FRT_HIP(hipMemsetAsync(G.gwork, 0, kGatherGroups * 64 * sizeof(unsigned), h->stream));
-                    // the requests in the spatial order of their points from 4096 of them (FRT_GATHER_SORT=0: gather
-                    // order, =1: sorted at any count)
-                    static const int sort_mode = std::getenv("FRT_GATHER_SORT") ? std::atoi(std::getenv("FRT_GATHER_SORT")) : -1;
                     const uint32_t* perm = nullptr;
-                    if (sort_mode != 0 && (rays >= 4096 || sort_mode == 1) && rays < (int64_t)0x7FFFFFFF) {
-                        if (grow(&G.gkeys, G.gkeys_cap, 4 * rays)) return -1;
-                        uint32_t *k0 = G.gkeys, *k1 = G.gkeys + rays, *i0 = G.gkeys + 2 * rays, *i1 = G.gkeys + 3 * rays;
-                        hipLaunchKernelGGL(k_gather_keys, dim3(grid_for(rays)), dim3(kBlock), 0, h->stream, h->S, G.greq, rays,
-                                           k0, i0);
+                    if (sorted) {
                         size_t tmp_bytes = 0;
-                        FRT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, i0, i1, (int)rays, 0, 31,
-                                                                   h->stream));
+                        FRT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, i0, i1, (int)rays, 0,
+                                                                   kGatherKeyBits, h->stream));
                         if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
                         FRT_HIP(hipcub::DeviceRadixSort::SortPairs((void*)h->scan_tmp, tmp_bytes, k0, k1, i0, i1, (int)rays, 0,
-                                                                   31, h->stream));
+                                                                   kGatherKeyBits, h->stream));
                         perm = i1;
                     }
                     int cus = 0;
