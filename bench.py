@@ -338,19 +338,19 @@ def gather_roofline(gd: dict) -> dict:
     rate (not HBM), and `issue` holds the VALU / SALU issue rates of the PMC pass over the live launch time."""
     n = gd["sub_launches"]["k_gather_est"]
     avg_ms = gd["sub_ms"]["k_gather_est"] / n
-    roof = {"bound": "valu-issue", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+    roof = {"bound": "valu-issue", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
             "kernel": "k_gather_est", "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": n,
-            "bytes_model": "L2-request bytes: the byte model counts every byte the estimate requests from the memory "
-                           "system (candidate positions, photon records, request, result); with the requests in "
-                           "spatial order they hit the XCDs' L2, so this is not HBM traffic and frac is not an HBM "
-                           "fraction (traffic is the HBM side)"}
+            "bytes_model": "l2_request_gbs: the byte model counts every byte the estimate requests from the memory "
+                           "system (candidate positions, photon records, request, result) over the live launch time; "
+                           "with the requests in spatial order they hit the XCDs' L2, so it is not an HBM rate "
+                           "(traffic is the HBM side). achieved / peak / frac: the VALU issue rate"}
     model = os.path.join(ROOT, "profiles", "r03_gi_estimate_counters.json")
     if os.path.exists(model):
         m = json.load(open(model))
         per_query = m["algorithmic_bytes_per_query"]
         per_launch = per_query * gd["gather_rays"] / n
         ach = per_launch / (avg_ms * 1e-3) / 1e9
-        roof.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+        roof.update({"l2_request_gbs": round(ach, 1),
                      "algorithmic_bytes_per_query": round(per_query, 1),
                      "algorithmic_bytes_per_launch": round(per_launch),
                      "candidates_per_query": round(m["candidates_read_per_query"], 1),
@@ -369,6 +369,9 @@ def gather_roofline(gd: dict) -> dict:
                      "salu_insts_per_query": round(t["SQ_INSTS_SALU_per_launch"] / queries, 1),
                      "wait_any_frac": round(t.get("sq_wait_any_frac_of_wave_cycles", 0.0), 3),
                      "issue": issue_block(t, avg_ms, queries, "queries")})
+        v = roof["issue"].get("valu")
+        if v:  # achieved / peak / frac: the VALU issue rate of the PMC pass over the live launch time
+            roof.update({"achieved": v["achieved"], "peak": v["peak"], "unit": v["unit"], "frac": v["frac"]})
         if "TCC_HIT_sum_per_launch" in t and "TCC_MISS_sum_per_launch" in t:
             hm = t["TCC_HIT_sum_per_launch"] + t["TCC_MISS_sum_per_launch"]
             roof["l2_hit_rate"] = round(t["TCC_HIT_sum_per_launch"] / hm, 4) if hm else None

@@ -407,9 +407,12 @@ __device__ __forceinline__ void radix_pick(const unsigned* c4, unsigned need, un
     below = (unsigned)__builtin_amdgcn_readlane((int)b, owner);
 }
 
-// the sum passes' record chunks in flight per round trip (80 bytes per lane each)
+// the sum passes' record chunks in flight per round trip (80 bytes per lane each). 1 since round 5: with the final
+// gather's requests in spatial order the records are L2 hits, and a second chunk's 20 VGPRs cost more than its
+// overlap saves (k_gather_est 1401 -> 1293 ms per cornell_gi_480x270_8x8 frame, 27 -> 12 spilled VGPRs,
+// profiles/r05_ab_gi_sort.txt); the lane's records are summed in the same order either way
 #ifndef FRT_SUM_CHUNKS
-#define FRT_SUM_CHUNKS 2
+#define FRT_SUM_CHUNKS 1
 #endif
 constexpr int kSumChunks = FRT_SUM_CHUNKS;
 
