@@ -699,16 +699,26 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     const int ns = L.num_samples;
                     // a wave-uniform row: the same point in every lane, so its address is wave-uniform and the loads go
                     // through the scalar cache (the point's coordinates in SGPRs, no vector memory latency)
+                    // (the constant address space: without it the compiler cannot prove that nothing the kernel stores
+                    // aliases the points, and emits vector flat loads of the uniform address, waited on every point)
+#ifndef FRT_SHADE_CONST_PTS
+#define FRT_SHADE_CONST_PTS 1
+#endif
+#if FRT_SHADE_CONST_PTS
+                    using const_pts = const __attribute__((address_space(4))) double*;
+#else
+                    using const_pts = const double*;
+#endif
                     auto uniform_points = [&](const double* up) {
-                        const double* sp = (const double*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                                                                (int)(uint32_t)(uint64_t)up)) |
-                                                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                                                                 (int)(uint32_t)((uint64_t)up >> 32))
-                                                             << 32));
+                        const const_pts sp = (const_pts)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                              (int)(uint32_t)(uint64_t)up)) |
+                                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                               (int)(uint32_t)((uint64_t)up >> 32))
+                                                           << 32));
                         double a[3] = {sp[0], sp[1], sp[2]};
                         for (int p = 0; p < ns; ++p) {  // (the next point's scalar loads ahead of this one's arithmetic)
                             const double lp[3] = {a[0], a[1], a[2]};
-                            const double* q = sp + 3 * min(p + 1, ns - 1);
+                            const const_pts q = sp + 3 * min(p + 1, ns - 1);
                             a[0] = q[0];
                             a[1] = q[1];
                             a[2] = q[2];
