@@ -97,6 +97,9 @@ struct NodeCols {
     Cols<NodeColors> col;
     const ShadowHead* head = nullptr;  // over_point, key (the level's ShadowHead array)
     int32_t root = 0;                  // level 0: parent / slot are -1 / 0 and not stored
+    // level 0 of a scene without GI: eyev is the camera ray's direction negated, which its one reader (shade_node,
+    // through camera_eyev) recomputes from the node's sample; its 24 bytes per node are not stored
+    int32_t eye_cam = 0;
     static size_t bytes(int64_t cap) { return Cols<NodeCore>::bytes(cap) + Cols<NodeColors>::bytes(cap); }
     void set(uint64_t* base, int64_t cap) {  // (host) one allocation of bytes(cap)
         core.w = base;
@@ -122,7 +125,11 @@ struct NodeCols {
         core.w[i] = t[0];
         if (!root) core.w[cap + i] = t[1];
 #pragma unroll
-        for (int f = 2; f < 8; ++f) core.w[f * cap + i] = t[f];
+        for (int f = 2; f < 5; ++f) core.w[f * cap + i] = t[f];
+        if (!eye_cam) {
+#pragma unroll
+            for (int f = 5; f < 8; ++f) core.w[f * cap + i] = t[f];
+        }
         if (own_d) core.w[8 * cap + i] = t[8];
         if (c.flags & kMix) core.w[9 * cap + i] = t[9];
         if (own_colors) {
@@ -148,7 +155,9 @@ struct NodeCols {
         t[0] = core.w[i];
         t[1] = root ? (uint64_t)(uint32_t)-1 : core.w[cap + i];
 #pragma unroll
-        for (int f = 2; f < 8; ++f) t[f] = core.w[f * cap + i];
+        for (int f = 2; f < 5; ++f) t[f] = core.w[f * cap + i];
+#pragma unroll
+        for (int f = 5; f < 8; ++f) t[f] = eye_cam ? 0ull : core.w[f * cap + i];  // (eye_cam: camera_eyev)
         const int32_t mat = (int32_t)(uint32_t)t[0], fl = (int32_t)(t[0] >> 32);
         const double od = (fl & kOwnD) ? __longlong_as_double((long long)core.w[8 * cap + i])
                           : mat >= 0 ? 1.0 - mats[mat].Tr : 0.0;
@@ -566,6 +575,16 @@ __device__ __forceinline__ double dot3_shade(const double* a, const double* b) {
     if (FRT_SHADE_FMA) return __builtin_fma(a[0], b[0], __builtin_fma(a[1], b[1], a[2] * b[2]));
     return dot3(a, b);
 }
+// a level-0 node's eyev where the level does not store it (NodeCols::eye_cam): prepare_computations' negated ray
+// direction (frt_shade.hpp prepare) of the node's camera ray, the same camera_ray k_prepare traced, bit for bit
+__device__ __forceinline__ void camera_eyev(const DevScene& S, const Batch& B, int64_t i, double* eyev) {
+    Ray r;
+    uint64_t key;
+    unsigned ce = 0;
+    camera_ray(S, B, i, r, key, ce);
+    for (int k = 0; k < 3; ++k) eyev[k] = r.d[k] * -1.0;
+}
+
 // lighting_microfacet (renderer.c:895-979) per light, summed as shade_hit does (renderer.c:704-725): the
 // A, D, S triples of path node i into out (out[4k + c]: term k, channel c)
 // (lds_row: k_shade_lit's per-wave LDS staging of a multi-row light's row, kLdsPoints points; nullptr elsewhere)
@@ -850,6 +869,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
     }
     if (!kLazy && mine && !heavy) {
         double out[12];
+        if (rec.eye_cam) camera_eyev(S, B, i, nr.eyev);
         shade_node(S, B, nr, i, counts, out);
         tri_store(surface, i, out);
     }
@@ -933,7 +953,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
         if (m >= total) return;
         i = (int64_t)lit[slot];
     }
-    const NodeRec nr = rec.load(i, S.materials);
+    NodeRec nr = rec.load(i, S.materials);
+    if (rec.eye_cam) camera_eyev(S, B, i, nr.eyev);
     double out[12];
     if (kRows) {
         __shared__ double lds_rows[kBlock / 64][3 * kLdsPoints];  // (a multi-row light's row per wave, 3 KB)
@@ -3014,6 +3035,9 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
         FRT_HIP(hipMalloc(&p, frt::NodeCols::bytes(nc)));
         L.rec.set((uint64_t*)p, nc);
         L.rec.root = d == 0 ? 1 : 0;
+        // (FRT_EYE_CAM=0: level 0 stores eyev too, A/B runs)
+        static const bool eye_cam_env = !(std::getenv("FRT_EYE_CAM") && std::atoi(std::getenv("FRT_EYE_CAM")) == 0);
+        L.rec.eye_cam = d == 0 && !h->S.cfg.use_gi && eye_cam_env ? 1 : 0;
     }
     FRT_HIP(hipMalloc((void**)&L.head, nc * sizeof(frt::ShadowHead)));
     L.rec.head = L.head;

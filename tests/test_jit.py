@@ -179,6 +179,19 @@ def test_jit_closest_hit_equals_generic_walk(built, name, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "reflect_refract_test_150", "checkered_sphere_dof_100",
+                                  "checkered_sphere_jitter_100", "cornell_shipped_48_4x4", "patterns_160x80"])
+def test_level0_eyev_from_camera_equals_stored(built, name, tmp_path):
+    """Level 0 of a scene without GI does not store its nodes' eye vectors (NodeCols::eye_cam): the shading recomputes
+    each one from the node's camera ray (camera_eyev: jitter and thin-lens apertures included). The canvas equals the
+    one that stores them (FRT_EYE_CAM=0), bit for bit."""
+    ref, _ = _render_env_process(name, {"FRT_EYE_CAM": "0"}, tmp_path / "s.npy")
+    img, _ = _render_env_process(name, {}, tmp_path / "c.npy")
+    assert np.isfinite(img).all()
+    assert np.array_equal(img, ref), name
+
+
+@pytest.mark.gpu
 def test_tile_kernels_on_shipped_multi_row_light(built, tmp_path):
     """The reference's shipped light (cornell_box.yml: 65 535 jittered cache rows, each path node drawing its own row):
     the tile, sub-part and sub-tile stages decide beams against part boxes that hold for every row (CMJ keeps sample
