@@ -3359,7 +3359,11 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         stream_sync(h) != hipSuccess)
                         return;
                     uint64_t listed_s = 0;
-                    const bool subtiled = h->jit_subtile && h->subtile > 0 && h->subtile < h->tile && h->stbox;
+                    // (FRT_JIT_SUBTILE_DEEP=0: levels past the camera's walk the sub-part list ray by ray, A/B runs)
+                    static const bool subtile_deep =
+                        !(std::getenv("FRT_JIT_SUBTILE_DEEP") && std::atoi(std::getenv("FRT_JIT_SUBTILE_DEEP")) == 0);
+                    const bool subtiled = h->jit_subtile && h->subtile > 0 && h->subtile < h->tile && h->stbox &&
+                                          (B.level == 0 || subtile_deep);
                     const uint64_t nst = subtiled ? (uint64_t)(h->tile / h->subtile) : 0;
                     list_blocks = seg_table(h->host_mcount, ssegcap, subtiled ? nst : (uint64_t)h->tile, tseg, listed_s);
                     h->sub_pairs += listed * (uint64_t)h->sub;

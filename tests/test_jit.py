@@ -156,7 +156,7 @@ def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
                              {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"},
                              # the sub-tile (sub-part) stage's list walked ray by ray without the node pair kernel
                              {"FRT_JIT_NODE_BEAM": "0"}, {"FRT_JIT_NODE_BEAM": "0", "FRT_JIT_SUBTILE": "0"},
-                             {"FRT_JIT_NODE_BEAM": "1"})):
+                             {"FRT_JIT_NODE_BEAM": "1"}, {"FRT_JIT_SUBTILE_DEEP": "0"})):
         img, st = _render_env_process(name, env, tmp_path / ("j%d.npy" % i))
         assert st[0] == 1 and st[1] > 0, (env, st)
         if env.get("FRT_JIT_SUB") != "0":
