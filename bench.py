@@ -208,7 +208,8 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
     """The per-ray shadow kernel (frt_jit_shadow; the generic k_shadow when the scene is not eligible),
     timed by HIP events around its own launches (frt_frame_stats.sub_ms). Algorithmic bytes (engine-side
     shadow_kernel_bytes): per list entry its 8 bytes, per node of an entry its 40-byte ShadowHead once (not per ray:
-    the node's rays share it) and one 4-byte count, per ray of a multi-row light its 24-byte point.
+    the node's rays share it; and at most once per node and launch: the entries of one tile re-read their nodes'
+    records from L2) and one 4-byte count, per ray of a multi-row light its 24-byte point.
 
     bound: "valu-issue" — the kernel moves few bytes (achieved / peak / frac below are its algorithmic
     HBM bytes against the 8 TB/s peak, as the bench contract asks) and is limited by instruction issue on

@@ -3529,7 +3529,9 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         hip_ignore(hipMemsetAsync(h->redo_count, 0, sizeof(unsigned), h->stream));
         h->rays_walked += total_mixed * lpp;  // (parts of fewer samples count their padding lanes too)
         h->pairs_walked += total_mixed;
-        h->heads_walked += direct_in ? total_mixed * direct_nodes : total_mixed;  // (ShadowHeads read: a node per lane group)
+        // (ShadowHeads read: a node per lane group, each of the level's n nodes at most once per launch — the entries of
+        // one tile re-read its nodes' records from L2)
+        h->heads_walked += std::min<uint64_t>(direct_in ? total_mixed * direct_nodes : total_mixed, (uint64_t)n);
         KTimer tr(h, h->cur_st, 9);
         // the mixed pairs' blocks by segment (jit::SegTable); every pair in order without the pair kernel
         frt::jit::SegTable seg{};
@@ -4570,8 +4572,9 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         st->hits = hits;
         st->shadow_rays = h->S.cfg.include_direct ? hits * (uint64_t)h->samples_per_node : 0;
         // DESIGN.md byte model of the per-ray shadow kernel: per list entry its 4-byte entry and 4-byte resume word;
-        // per node of an entry its ShadowHead, read once for the entry's rays (heads_walked: an entry of the sub-part
-        // list holds a tile's 64 nodes, of the node-pair list one), and one 4-byte count added; with a multi-row light
+        // per node of an entry its ShadowHead, read once for the entry's rays and at most once per launch for the node
+        // (heads_walked: an entry of the sub-part list holds a tile's 64 nodes, of the node-pair list one), and one
+        // 4-byte count added; with a multi-row light
         // each ray's 24-byte point from its node's row (a single-row light's points stay in cache); the generic walk:
         // per shaded node the ShadowHead + one 4-byte count per light
         constexpr double kHead = (double)sizeof(frt::ShadowHead);
