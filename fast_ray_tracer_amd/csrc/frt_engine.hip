@@ -1040,8 +1040,15 @@ __global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(DevScene S, cons
                                                                 Cols<Tri9> child, int32_t spp, int32_t ppb,
                                                                 int64_t npix, const frt_material* __restrict__ mats,
                                                                 int32_t include_specular, double* __restrict__ out) {
+    // (each pixel's column sum goes back into the first slot of the run it was summed from: only the thread that
+    // summed a run reads it, and the block's LDS stays at 18.5 KB, so six blocks fit a CU instead of four)
+#ifndef FRT_RESOLVE_INPLACE
+#define FRT_RESOLVE_INPLACE 1
+#endif
     __shared__ double stage[9][kFuseBlock + 1];
-    __shared__ double sum[9][kFuseBlock];
+#if !FRT_RESOLVE_INPLACE
+    __shared__ double sum_sep[9][kFuseBlock];
+#endif
     const int t = threadIdx.x;
     const int64_t p0 = (int64_t)blockIdx.x * ppb;
     const int64_t i = p0 * spp + t;
@@ -1059,9 +1066,18 @@ __global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(DevScene S, cons
         const double* st = stage[f] + lp * spp;
         double acc = 0.0;
         for (int kk = 0; kk < spp; ++kk) acc += st[kk];
-        sum[f][lp] = acc * (1.0 / (double)spp);
+#if FRT_RESOLVE_INPLACE
+        stage[f][lp * spp] = acc * (1.0 / (double)spp);
+#else
+        sum_sep[f][lp] = acc * (1.0 / (double)spp);
+#endif
     }
     __syncthreads();
+#if FRT_RESOLVE_INPLACE
+    auto sum = [&](int f, int lp) { return stage[f][lp * spp]; };
+#else
+    auto sum = [&](int f, int lp) { return sum_sep[f][lp]; };
+#endif
     for (int q = t; q < ppb * 4; q += kFuseBlock) {
         const int lp = q >> 2, f = q & 3;
         const int64_t p = p0 + lp;
@@ -1071,9 +1087,9 @@ __global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(DevScene S, cons
             o[3] = 0.0;
             continue;
         }
-        double v = 0.0 + sum[f][lp];  // (A + D + S) / 3 of channel f
-        v += sum[3 + f][lp];
-        v += sum[6 + f][lp];
+        double v = 0.0 + sum(f, lp);  // (A + D + S) / 3 of channel f
+        v += sum(3 + f, lp);
+        v += sum(6 + f, lp);
         v *= 1.0 / 3.0;
         o[f] = v;
     }
