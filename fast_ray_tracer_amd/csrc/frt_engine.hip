@@ -2551,22 +2551,40 @@ int frt_photon_pass_stats(int64_t* out, int n) {
 size_t frt_frame_stats_size(void) { return sizeof(frt_frame_stats); }
 
 int frt_device_warmup(int device) {
+    // (FRT_WARMUP_TRACE: each step's time to stderr)
+    static const bool trace = std::getenv("FRT_WARMUP_TRACE") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!trace) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "frt warmup: %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    };
     if (hipSetDevice(device) != hipSuccess) {
         (void)hipGetLastError();
         return -1;
     }
+    mark("hipSetDevice");
     hip_ignore(hipFree(nullptr));  // (creates the context)
+    mark("context");
     // the first allocation, copies both ways and kernel launch of a process set up the runtime's memory pools,
     // staging buffers and this library's code object on the device: paid here, beside the caller's work
     void* p = nullptr;
     if (hipMalloc(&p, 1 << 20) == hipSuccess) {
+        mark("hipMalloc");
         hipStream_t s = nullptr;
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+            mark("stream");
             unsigned host[64] = {0};
             hip_ignore(hipMemcpyAsync(p, host, sizeof(host), hipMemcpyHostToDevice, s));
+            hip_ignore(hipStreamSynchronize(s));
+            mark("H2D copy");
             hipLaunchKernelGGL(k_warm, dim3(1), dim3(64), 0, s, (unsigned*)p);
+            hip_ignore(hipStreamSynchronize(s));
+            mark("first kernel (code object load)");
             hip_ignore(hipMemcpyAsync(host, p, sizeof(host), hipMemcpyDeviceToHost, s));
             hip_ignore(hipStreamSynchronize(s));
+            mark("D2H copy");
             hip_ignore(hipStreamDestroy(s));
         }
         hip_ignore(hipFree(p));
