@@ -2550,6 +2550,11 @@ int frt_photon_pass_stats(int64_t* out, int n) {
 
 size_t frt_frame_stats_size(void) { return sizeof(frt_frame_stats); }
 
+// a stream frt_device_warmup created, handed to the device's next frt_scene_upload (a process's first streams cost
+// 10-160 ms each: tools/warmup_probe.py, profiles/r05_warmup_probe.txt)
+static std::mutex g_warm_mu;
+static hipStream_t g_warm_stream[64] = {};
+
 int frt_device_warmup(int device) {
     // (FRT_WARMUP_TRACE: each step's time to stderr)
     static const bool trace = std::getenv("FRT_WARMUP_TRACE") != nullptr;
@@ -2573,7 +2578,9 @@ int frt_device_warmup(int device) {
     if (hipMalloc(&p, 1 << 20) == hipSuccess) {
         mark("hipMalloc");
         hipStream_t s = nullptr;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+        // (FRT_WARMUP_MODE=1: the null stream instead of a stream of its own, probes only)
+        static const int wmode = std::getenv("FRT_WARMUP_MODE") ? std::atoi(std::getenv("FRT_WARMUP_MODE")) : 0;
+        if (wmode == 1 || hipStreamCreate(&s) == hipSuccess) {  // (the handle's kind of stream: it may take it)
             mark("stream");
             unsigned host[64] = {0};
             hip_ignore(hipMemcpyAsync(p, host, sizeof(host), hipMemcpyHostToDevice, s));
@@ -2585,7 +2592,11 @@ int frt_device_warmup(int device) {
             hip_ignore(hipMemcpyAsync(host, p, sizeof(host), hipMemcpyDeviceToHost, s));
             hip_ignore(hipStreamSynchronize(s));
             mark("D2H copy");
-            hip_ignore(hipStreamDestroy(s));
+            if (s) {
+                std::lock_guard<std::mutex> lk(g_warm_mu);
+                if (device >= 0 && device < 64 && g_warm_stream[device] == nullptr) g_warm_stream[device] = s;
+                else hip_ignore(hipStreamDestroy(s));
+            }
         }
         hip_ignore(hipFree(p));
     }
@@ -2932,7 +2943,20 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         return fail("frt_scene_upload: debug counters");
     }
 #endif
-    if (hipStreamCreate(&h->stream) != hipSuccess || hipMalloc((void**)&h->counters, frt::kQueueSegs * frt::kCounterLine * sizeof(unsigned long long)) != hipSuccess ||
+    static const bool wtrace = std::getenv("FRT_WARMUP_TRACE") != nullptr;
+    const auto ts0 = std::chrono::steady_clock::now();
+    {
+        std::lock_guard<std::mutex> lk(g_warm_mu);
+        if (device >= 0 && device < 64 && g_warm_stream[device] != nullptr) {
+            h->stream = g_warm_stream[device];  // (frt_device_warmup's)
+            g_warm_stream[device] = nullptr;
+        }
+    }
+    const bool stream_ok = h->stream != nullptr || hipStreamCreate(&h->stream) == hipSuccess;
+    if (wtrace)
+        std::fprintf(stderr, "frt upload: hipStreamCreate %.2f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count());
+    if (!stream_ok || hipMalloc((void**)&h->counters, frt::kQueueSegs * frt::kCounterLine * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&h->err, sizeof(unsigned)) != hipSuccess || hipEventCreate(&h->ev[0]) != hipSuccess ||
         hipEventCreate(&h->ev[1]) != hipSuccess) {
         frt_scene_release(h);

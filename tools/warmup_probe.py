@@ -16,11 +16,11 @@ PROBE = ("import sys, time, json; sys.path.insert(0, %r); from fast_ray_tracer_a
          % (ROOT, os.path.join(GOLDEN, "scenes", "cornell_direct_1920x1080_8x8.c"), os.path.join(GOLDEN, "assets")))
 
 
-def run(tag):
+def run(tag, extra=None):
     for i in range(3):
         p = subprocess.run([sys.executable, "-c", PROBE], capture_output=True, text=True, timeout=300,
-                           env=dict(os.environ, FRT_WARMUP_TRACE="1"))
-        lines = [ln for ln in (p.stdout + p.stderr).splitlines() if ln.startswith(("RM", "PH", "frt warmup"))]
+                           env=dict(os.environ, FRT_WARMUP_TRACE="1", **(extra or {})))
+        lines = [ln for ln in (p.stdout + p.stderr).splitlines() if ln.startswith(("RM", "PH", "frt warmup", "frt upload"))]
         print("%s run %d (rc %d): %s" % (tag, i, p.returncode, " | ".join(lines)), flush=True)
 
 
