@@ -751,8 +751,8 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     } else if (__ballot(row != ra) == 0ull && lds_row != nullptr) {
                         // the wave shares its row (the lit list in row order): the row into the wave's LDS in one
                         // coalesced round trip by the active lanes, then every lane reads the same point (a broadcast).
-                        // Through the scalar cache instead, every point was a trip to L2: the waves of a CU read
-                        // different rows, more than the scalar cache holds.
+                        // (Measured slower than the scalar loads below once those were real scalar loads: the LDS
+                        // reads' latency is paid on every point, the scalar loads run a point ahead.)
                         const double* rp = row0 + 3 * (int64_t)ra * ns;
                         const unsigned long long act = __ballot(true);
                         const int lane = (int)(threadIdx.x & 63);
@@ -956,7 +956,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     NodeRec nr = rec.load(i, S.materials);
     if (rec.eye_cam) camera_eyev(S, B, i, nr.eyev);
     double out[12];
-    if (kRows) {
+// FRT_SHADE_LDS_ROWS=1: a wave's shared row staged through LDS (A/B runs). 0 (default): read through the scalar
+// cache like the single-row light's points, 14.2 -> 13.1 ms per shipped frame (profiles/r05_ab_shade_scalar_rows.txt)
+#ifndef FRT_SHADE_LDS_ROWS
+#define FRT_SHADE_LDS_ROWS 0
+#endif
+    if (kRows && FRT_SHADE_LDS_ROWS) {
         __shared__ double lds_rows[kBlock / 64][3 * kLdsPoints];  // (a multi-row light's row per wave, 3 KB)
         shade_node(S, B, nr, i, counts, out, lds_rows[threadIdx.x >> 6]);
     } else {
