@@ -1560,8 +1560,10 @@ constexpr int kGatherEstCap = FRT_GATHER_CAP;
 #ifndef FRT_EST_WAVES
 #define FRT_EST_WAVES 4
 #endif
+// (one wave per block since round 5: with the requests in spatial order, 4 / 2 / 8 waves per block measured 20.76 s
+// of estimate per 1920x1080 GI frame against 20.28 s with 1, profiles/r05_ab_gi_sort.txt)
 #ifndef FRT_GATHER_WAVES_PER_BLOCK
-#define FRT_GATHER_WAVES_PER_BLOCK 4
+#define FRT_GATHER_WAVES_PER_BLOCK 1
 #endif
 constexpr int kGatherWavesPerBlock = FRT_GATHER_WAVES_PER_BLOCK;
 #ifndef FRT_GATHER_REQ_PER_WAVE
