@@ -4549,7 +4549,11 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 }
                 if (split) {
                     KTimer tl(h, st, 15);  // (inside the shade slot: k_shade_lit alone, sub_ms[7])
-                    hipLaunchKernelGGL(sorted ? k_shade_lit<true> : k_shade_lit<false>, dim3(grid_for(n)), dim3(kBlock), 0,
+#ifndef FRT_SHADE_LIT_BLOCK
+#define FRT_SHADE_LIT_BLOCK 64  // (one wave per block: 9.15 -> 8.83 ms per headline frame, profiles/r05_ab_shade_block.txt; <= kBlock)
+#endif
+                    hipLaunchKernelGGL(sorted ? k_shade_lit<true> : k_shade_lit<false>, dim3(grid_for(n, FRT_SHADE_LIT_BLOCK)),
+                                       dim3(FRT_SHADE_LIT_BLOCK), 0,
                                        h->stream, h->S, B, L.rec, L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap,
                                        sorted ? (const uint32_t*)h->lit_flat : nullptr);
                 }
