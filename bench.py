@@ -15,7 +15,10 @@ One step = one full frame: every rank renders its interleaved rows on its GPU
 Metric: Mrays/s of rays actually traced (primary + secondary + shadow), summed
 over ranks, plus wall-clock per frame; reference-equivalent Mrays/s (the rays the
 reference would cast, counted by the oracle: zero-weight secondary subtrees
-included) are reported beside it.
+included) are reported beside it. `value` counts every shadow ray, also the ones
+the beam stages decide for a whole beam at once; `walked_mrays_s` counts only the
+rays walked one by one, and ms_per_step / reference_equivalent_mrays_s are the
+figures to compare with the reference.
 
 Also on the same JSON line:
   shipped          the shipped direct-lighting configuration (cornell_box.yml's 65 535-row jittered light cache, GI
@@ -25,8 +28,11 @@ Also on the same JSON line:
                    new seed so photon tracing + map build run inside the timed region
   render_multi_*   wall time of the drop-in entry point itself (flatten, upload, hiprtc
                    compile of the scene kernel, render, copy to the host canvas)
-  roofline         the dominant kernel (the shadow pass) against HBM peak, with the PMC
-                   traffic / VALU counters committed under profiles/
+  roofline         the frame's dominant kernel by live HIP-event time (k_shade_lit on the headline) against the
+                   peak of the bound its committed PMC pass shows (binary64 FLOPs against the 78.6 TFLOP/s vector
+                   peak, instruction issue, or HBM bytes against 8 TB/s); a PMC pass is used only when it was
+                   measured on this tree's device sources and its rocprof launch time lies within 20 % of the live
+                   one (latest_pmc), otherwise the fields are null and pmc_rejected says why
   cpu_baseline     the reference's own pthread render_multi on this host's cores, on a
                    bounded sample of the same workload (the same camera at 240x135)
 
@@ -172,18 +178,63 @@ def cpu_baseline(all_threads: bool = False) -> dict | None:
                       % (CPU_SAMPLE_SCENE, threads, total)}
 
 
-def latest_pmc(kernel: str, workload: str):
-    """The newest committed PMC summary (profiles/rNN_pmc_*.json) of this kernel on this workload."""
-    best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json"))):
+PROFILES = os.path.join(ROOT, "profiles")
+# the device library's sources: a PMC summary is evidence for the kernels these files compiled to, so
+# tools/pmc_summary.py stamps it with their hash and a summary of other sources is not paired with a live time
+DEVICE_SOURCES = [os.path.join(ROOT, "include", "frt_device.h")] + [
+    os.path.join(ROOT, "fast_ray_tracer_amd", "csrc", f) for f in
+    ("frt_camera.hpp", "frt_cols.hpp", "frt_engine.hip", "frt_gi.hpp", "frt_jit.h", "frt_jit.hip", "frt_jit_rt.hpp",
+     "frt_math.hpp", "frt_shade.hpp", "frt_shadow.hpp", "frt_traverse.hpp")]
+# a PMC pass's rocprof launch time may differ from the live HIP-event time by this much (relative) and still be
+# paired with it: more means another build, another workload or another box state, and its rates would be fiction
+PMC_TIME_TOL = 0.20
+
+
+def device_source_sha(paths=None) -> str:
+    """sha256 (first 16 hex digits) over the device sources' names and bytes."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(paths or DEVICE_SOURCES):
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def latest_pmc(kernel: str, workload: str, live_avg_ms: float | None = None, profiles_dir: str | None = None):
+    """The newest committed PMC summary (profiles/rNN_pmc_*.json) of this kernel on this workload that may be
+    paired with a live launch time: it must carry the hash of the device sources it was measured on
+    (device_source_sha16, written by tools/pmc_summary.py) equal to this tree's, and its rocprof average launch
+    time must lie within PMC_TIME_TOL of live_avg_ms. Returns (path, summary, None), or (None, None, reason)
+    when no summary qualifies (reason: why the newest candidate was rejected)."""
+    cands = []
+    for p in sorted(glob.glob(os.path.join(profiles_dir or PROFILES, "r*_pmc_*.json"))):
         try:
             t = json.load(open(p))
         except (OSError, ValueError):
             continue
         # (older summaries name the kernel by the regex their pass used, "k_shadow<")
         if t.get("kernel", "").rstrip("<") == kernel and t.get("workload") == workload:
-            best = (p, t)
-    return best
+            cands.append((p, t))
+    if not cands:
+        return None, None, "no PMC summary of %s on %s under profiles/" % (kernel, workload)
+    sha = device_source_sha()
+    reasons = []
+    for p, t in reversed(cands):
+        name = os.path.basename(p)
+        if t.get("device_source_sha16") != sha:
+            reasons.append("%s: measured on other device sources (%s, this tree %s)"
+                           % (name, t.get("device_source_sha16", "no source hash"), sha))
+            continue
+        ra = t.get("rocprof_avg_ms")
+        if live_avg_ms is not None:
+            if not ra or not live_avg_ms or abs(ra - live_avg_ms) > PMC_TIME_TOL * live_avg_ms:
+                reasons.append("%s: rocprof launch %s ms vs live %.4f ms (more than %d %% apart)"
+                               % (name, ("%.4f" % ra) if ra else "n/a", live_avg_ms or 0.0, round(100 * PMC_TIME_TOL)))
+                continue
+        return p, t, None
+    return None, None, reasons[0]
 
 
 def issue_block(t: dict, avg_ms: float, units_per_launch: float, unit_name: str) -> dict:
@@ -231,9 +282,10 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
             "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": nl,
             "algorithmic_bytes_per_launch": round(per_launch),
             "timing": "HIP events around each launch on the engine stream (frt_frame_stats.sub_ms)"}
-    found = latest_pmc(kname, workload)
-    if found:
-        path, t = found
+    path, t, why = latest_pmc(kname, workload, avg_ms)
+    if why:
+        roof["pmc_rejected"] = why
+    if path:
         if "traffic_bytes_per_launch" in t:
             roof["traffic"] = round(t["traffic_bytes_per_launch"])
         else:  # FETCH_SIZE + WRITE_SIZE (tools/pmc_summary.py, KiB units already converted)
@@ -249,21 +301,23 @@ def shadow_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> 
     nb = d.get("sub_launches", {}).get("frt_jit_beam")
     tiled = bool(d.get("shadow_tile_pairs"))
     bname = "frt_jit_beam_list" if tiled else "frt_jit_beam"
-    fb = latest_pmc(bname, workload)
-    if nb and fb:
+    if nb:
         bavg = d["sub_ms"]["frt_jit_beam"] / nb
+        fp, ft, why = latest_pmc(bname, workload, bavg)
         pairs_per_launch = (d.get("shadow_pairs") or 0) / nb
-        roof.setdefault("issue", {})[bname] = dict(issue_block(fb[1], bavg, pairs_per_launch, "pairs"),
-                                                   avg_launch_ms=round(bavg, 4), source=os.path.relpath(fb[0], ROOT))
+        roof.setdefault("issue", {})[bname] = (
+            dict(issue_block(ft, bavg, pairs_per_launch, "pairs"), avg_launch_ms=round(bavg, 4),
+                 source=os.path.relpath(fp, ROOT)) if fp else {"avg_launch_ms": round(bavg, 4), "pmc_rejected": why})
     for kn, units, uname in (("frt_jit_tile", d.get("shadow_tile_pairs"), "tile_pairs"),
                              ("frt_jit_sub", d.get("shadow_sub_pairs"), "tile_sub_pairs"),
                              ("frt_jit_subtile", d.get("shadow_subtile_pairs"), "subtile_pairs")):
         nt = d.get("sub_launches", {}).get(kn)
-        ft = latest_pmc(kn, workload)
-        if nt and ft:
+        if nt:
             tavg = d["sub_ms"][kn] / nt
-            roof.setdefault("issue", {})[kn] = dict(issue_block(ft[1], tavg, (units or 0) / nt, uname),
-                                                    avg_launch_ms=round(tavg, 4), source=os.path.relpath(ft[0], ROOT))
+            fp, ft, why = latest_pmc(kn, workload, tavg)
+            roof.setdefault("issue", {})[kn] = (
+                dict(issue_block(ft, tavg, (units or 0) / nt, uname), avg_launch_ms=round(tavg, 4),
+                     source=os.path.relpath(fp, ROOT)) if fp else {"avg_launch_ms": round(tavg, 4), "pmc_rejected": why})
     return roof
 
 
@@ -297,11 +351,15 @@ def frame_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> d
     roof = {"kernel": pname, "avg_launch_ms": round(avg, 4), "launches_per_frame": nl, "ms_per_frame": round(ms, 3),
             "timing": "HIP events around each launch on the engine stream (frt_frame_stats)",
             "candidates_ms_per_frame": {k: round(v[0], 3) for k, v in sorted(cands.items(), key=lambda kv: -kv[1][0])}}
-    found = latest_pmc(pname, workload)
-    t = found[1] if found else {}
+    path, t, why = latest_pmc(pname, workload, avg)
+    found = path is not None
+    t = t or {}
     traffic = (t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)) if found else None
     f64 = [t.get("SQ_INSTS_VALU_%s_F64_per_launch" % x) for x in ("ADD", "MUL", "FMA", "TRANS")]
-    if found and all(v is not None for v in f64):
+    if not found:
+        # no counter evidence that matches this build and this launch time: nothing to divide, say why
+        roof.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "pmc_rejected": why})
+    elif all(v is not None for v in f64):
         flops = 64.0 * (f64[0] + f64[1] + f64[3]) + 128.0 * f64[2]
         ach = flops / (avg * 1e-3) / 1e12
         roof.update({"bound": "valu-fp64", "achieved": round(ach, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -317,7 +375,7 @@ def frame_roofline(d: dict, kernel_ms: dict, launches: dict, workload: str) -> d
                      "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None})
     roof["traffic"] = round(traffic) if traffic else None
     if found:
-        roof["source"] = os.path.relpath(found[0], ROOT)
+        roof["source"] = os.path.relpath(path, ROOT)
         roof["issue"] = issue_block(t, avg, 1.0, "launch")
         if "rocprof_avg_ms" in t:
             roof["rocprof_avg_launch_ms"] = round(t["rocprof_avg_ms"], 4)
@@ -357,9 +415,10 @@ def gather_roofline(gd: dict) -> dict:
                      "candidates_per_query": round(m["candidates_read_per_query"], 1),
                      "records_per_query": round(m["records_read_per_query"], 1),
                      "model_source": os.path.relpath(model, ROOT)})
-    found = latest_pmc("k_gather_est", GI_SCENE)
-    if found:
-        path, t = found
+    path, t, why = latest_pmc("k_gather_est", GI_SCENE, avg_ms)
+    if why:
+        roof["pmc_rejected"] = why
+    if path:
         traffic = 2.0 * t.get("fetch_size_bytes_per_launch", 0.0) + t.get("write_size_bytes_per_launch", 0.0)
         queries = gd["gather_rays"] / n
         roof.update({"traffic": round(traffic), "traffic_source": os.path.relpath(path, ROOT),

@@ -2,7 +2,8 @@
 """Summarise a profiling directory (tools/prof_shadow.sh): rocprof kernel stats of the kernel and every
 PMC pass's counters per launch of it. FETCH_SIZE / WRITE_SIZE (KiB) become bytes per launch; the
 MI355X guide's x2 correction for wide streaming reads is not applied (the shadow kernel's loads are
-8-byte broadcast loads).
+8-byte broadcast loads). The summary carries device_source_sha16, the hash of the device sources
+(bench.device_source_sha) the pass ran on.
 
   python tools/pmc_summary.py gpurun_out/prof_TAG frt_jit_shadow cornell_direct_1920x1080_8x8
 """
@@ -14,8 +15,13 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import device_source_sha  # noqa: E402  (bench.py's pairing rule: latest_pmc)
+
 out, kre, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-res = {"kernel": sys.argv[4] if len(sys.argv) > 4 else kre, "workload": workload}
+# the device sources this pass measured (bench.py pairs a summary only with live times of the same sources)
+res = {"kernel": sys.argv[4] if len(sys.argv) > 4 else kre, "workload": workload,
+       "device_source_sha16": device_source_sha()}
 for f in glob.glob(out + "/kt/**/*kernel_stats.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         if re.search(kre, row["Name"]):

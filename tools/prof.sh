@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 5: rocprofv3 kernel stats + PMC passes (one counter block set per pass) of a bench workload, summarised
+# rocprofv3 kernel stats + PMC passes (one counter block set per pass) of a bench workload, summarised
 # per kernel with tools/pmc_summary.py (run via gpurun from the repo root).
-#   tools/prof_r05.sh TAG SCENE "KERNEL1 KERNEL2 ..." [extra bench args]
+#   tools/prof.sh TAG SCENE "KERNEL1 KERNEL2 ..." [extra bench args]
 set -o pipefail
 TAG=$1; SC=$2; KS=$3; shift 3
 R=${GRAFT_REPO_ROOT:-$(pwd)}
