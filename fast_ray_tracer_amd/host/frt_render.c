@@ -253,7 +253,66 @@ static struct {
     int dev[64];
     frt_scene_handle *h[64];
     frt_scene fs;  /* the flattened scene they were uploaded from (owned) */
+    char *knobs;   /* the FRT_* environment at their upload (knob_signature; owned) */
 } g_kept;
+
+/* render_multi's process-wide state (g_kept, g_warmed, g_rm_phases, g_render_error) is used under this lock: two
+ * threads calling render_multi at once render one after the other instead of racing on the kept handles */
+static pthread_mutex_t g_rm_lock = PTHREAD_MUTEX_INITIALIZER;
+
+extern char **environ;
+
+/*
+ * The FRT_* environment, sorted, as one string: the engine reads its knobs (FRT_JIT, FRT_JIT_BEAM, FRT_MESH,
+ * FRT_SHADE_SORT, FRT_JIT_NODE_BEAM, FRT_EYE_CAM, the stage sizes, ...) when a scene is uploaded, so kept handles
+ * are reused only under the same knobs. The per-call variables (the device list, seed, stats path, this switch)
+ * are left out. Returns a malloc'd string (NULL when out of memory: then nothing is reused).
+ */
+static int
+cmp_str(const void *a, const void *b)
+{
+    return strcmp(*(const char *const *)a, *(const char *const *)b);
+}
+
+static char *
+knob_signature(void)
+{
+    static const char *const per_call[] = {"FRT_DEVICES=", "FRT_GPUS=", "FRT_DEVICE=", "FRT_SEED=", "FRT_STATS_OUT=",
+                                           "FRT_RM_KEEP="};
+    size_t n = 0, len = 1;
+    for (char **e = environ; e != NULL && *e != NULL; ++e) {
+        n += strncmp(*e, "FRT_", 4) == 0;
+    }
+    const char **v = (const char **)malloc((n ? n : 1) * sizeof(char *));
+    if (v == NULL) {
+        return NULL;
+    }
+    size_t m = 0;
+    for (char **e = environ; e != NULL && *e != NULL; ++e) {
+        if (strncmp(*e, "FRT_", 4) != 0) {
+            continue;
+        }
+        int skip = 0;
+        for (size_t q = 0; q < sizeof(per_call) / sizeof(per_call[0]); ++q) {
+            skip = skip || strncmp(*e, per_call[q], strlen(per_call[q])) == 0;
+        }
+        if (!skip && m < n) {
+            v[m++] = *e;
+            len += strlen(*e) + 1;
+        }
+    }
+    qsort(v, m, sizeof(char *), cmp_str);
+    char *out = (char *)malloc(len);
+    if (out != NULL) {
+        out[0] = '\0';
+        for (size_t q = 0; q < m; ++q) {
+            strcat(out, v[q]);
+            strcat(out, "\n");
+        }
+    }
+    free(v);
+    return out;
+}
 
 static int
 same_bytes(const void *a, const void *b, size_t n)
@@ -297,7 +356,22 @@ release_kept(void)
     if (g_kept.n > 0) {
         frt_flat_scene_free(&g_kept.fs);
     }
+    free(g_kept.knobs);
+    g_kept.knobs = NULL;
     g_kept.n = 0;
+}
+
+/*
+ * Release the handles render_multi keeps between calls (their device memory: the scene, the compiled kernels and
+ * the level state; a GI scene's gather buffers are GBs). The next render_multi uploads afresh. Safe to call at any
+ * time, also with nothing kept; the Python runtime calls it at exit and before it opens handles of its own.
+ */
+void
+frt_render_multi_release(void)
+{
+    pthread_mutex_lock(&g_rm_lock);
+    release_kept();
+    pthread_mutex_unlock(&g_rm_lock);
 }
 
 /* the phases of the last render_multi on this process, in ms (frt_render_multi_phases) */
@@ -346,8 +420,8 @@ warmup_worker(void *arg)
  * reference has no error return: on failure this logs the reason to stderr
  * and returns the (zeroed) canvas, as SURVEY.md 8(b) asks of a replacement.
  */
-Canvas
-render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
+static Canvas
+render_multi_locked(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
 {
     const double rm0 = now_ms();
     memset(g_rm_phases, 0, sizeof(g_rm_phases));
@@ -408,7 +482,9 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
     for (int k = 0; reuse && k < n; ++k) {
         reuse = g_kept.dev[k] == dev[k] && g_kept.h[k] != NULL;
     }
-    reuse = reuse && scenes_equal(&fs, &g_kept.fs);
+    char *knobs = knob_signature();
+    reuse = reuse && knobs != NULL && g_kept.knobs != NULL && strcmp(knobs, g_kept.knobs) == 0 &&
+            scenes_equal(&fs, &g_kept.fs);
     if (!reuse) {
         release_kept();
     }
@@ -520,23 +596,34 @@ render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
             }
             g_kept.fs = fs;
             memset(&fs, 0, sizeof(fs));
+            g_kept.knobs = knobs;
+            knobs = NULL;
         }
+    } else if (reuse) {
+        /* (a failed call keeps nothing. Reused: the jobs hold the kept handles or nothing (a job that was never
+         * set up), so every kept handle is released once through g_kept, whatever the jobs got to) */
+        release_kept();
     } else {
-        /* (a failed call keeps nothing: every job's handle, a reused one included, released once) */
         for (int k = 0; jobs != NULL && k < n; ++k) {
             if (jobs[k].h != NULL) {
                 frt_scene_release(jobs[k].h);
             }
         }
-        if (reuse) {
-            frt_flat_scene_free(&g_kept.fs);
-            g_kept.n = 0;
-        }
     }
+    free(knobs);
     free(jobs);
     free(th);
     frt_flat_scene_free(&fs);
     g_rm_phases[13] = now_ms() - rm0;
+    return c;
+}
+
+Canvas
+render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter)
+{
+    pthread_mutex_lock(&g_rm_lock);
+    Canvas c = render_multi_locked(cam, w, usteps, vsteps, jitter);
+    pthread_mutex_unlock(&g_rm_lock);
     return c;
 }
 

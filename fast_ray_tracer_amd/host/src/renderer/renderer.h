@@ -25,4 +25,10 @@
 Canvas render(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter);
 Canvas render_multi(Camera cam, World w, size_t usteps, size_t vsteps, bool jitter);
 
+/* frt extensions (no reference counterpart; main.c does not call them): the reason the last render_multi
+ * failed ("" after a successful call), and the release of the device handles render_multi keeps between calls
+ * for a repeat of the same scene (host/frt_render.c) */
+const char *frt_render_multi_error(void);
+void frt_render_multi_release(void);
+
 #endif

@@ -152,6 +152,8 @@ class GpuRenderer:
         self.lib = host_lib()
         if self.lib.frt_device_count() <= 0:
             raise RuntimeError("frt: no HIP device visible; the GPU path has no CPU fallback")
+        # the handles an earlier render_multi kept hold their device memory until released (GBs for a GI scene)
+        release_render_multi()
         self.scene = scene
         self.device = device
         h = self.lib.frt_host_prepare(scene.camera, scene.world, scene.usteps, scene.vsteps, scene.jitter, device)
@@ -242,9 +244,31 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
         lib.canvas_free(c)
     lib.frt_render_multi_error.restype = ctypes.c_char_p
     err = lib.frt_render_multi_error()
+    global _release_registered
+    if not _release_registered:  # (the kept handles go before the interpreter's teardown, not during it)
+        import atexit
+        lib.frt_render_multi_release.restype = None
+        atexit.register(lib.frt_render_multi_release)
+        _release_registered = True
     if err:
         raise RuntimeError("frt: render_multi failed: " + err.decode(errors="replace"))
     return out
+
+
+_release_registered = False
+
+
+def release_render_multi() -> None:
+    """Release the device handles render_multi keeps between calls (host/frt_render.c frt_render_multi_release:
+    the scene, its compiled kernels and level state on every device of the last call). Registered to run at exit."""
+    global _release_registered
+    lib = host_lib()
+    lib.frt_render_multi_release.restype = None
+    lib.frt_render_multi_release()
+    if not _release_registered:
+        import atexit
+        atexit.register(lib.frt_render_multi_release)
+        _release_registered = True
 
 
 RENDER_MULTI_PHASES = ("flatten", "upload", "upload.device_select", "upload.scene_buffers", "upload.walk_records_meshes",

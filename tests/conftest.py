@@ -13,7 +13,9 @@ if ORACLE_DIR not in sys.path:
 
 # The test scenes are small: every level of them would skip the shadow pass's beam stages (frt_engine.hip
 # launch_shadow: levels under FRT_JIT_MIN_PAIRS (node, light part) pairs walk their rays one by one). The tests
-# exercise the stages at every size; test_jit.py::test_small_levels_skip_beam_stages_bit_identical checks the default.
+# exercise the stages at every size; test_jit.py::test_small_levels_skip_beam_stages_bit_identical and
+# test_goldens_under_the_production_default (one golden per feature group, in processes without this override) check
+# the shipped default.
 os.environ.setdefault("FRT_JIT_MIN_PAIRS", "0")
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")

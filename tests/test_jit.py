@@ -131,8 +131,12 @@ def _render_env_process(name, env, out, **kw):
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
+    penv = dict(os.environ, **{k: v for k, v in env.items() if v is not None})
+    for k, v in env.items():  # (None: the variable unset, the engine's own default)
+        if v is None:
+            penv.pop(k, None)
     p = subprocess.run([sys.executable, "-c", _ENV_RENDER.format(tests=here, name=name, out=str(out), kw=kw)],
-                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
+                       env=penv, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     stats = [ln.split()[1:] for ln in p.stdout.splitlines() if ln.startswith("STATS")][-1]
     return np.load(str(out)), [int(x) for x in stats]
@@ -225,3 +229,28 @@ def test_small_levels_skip_beam_stages_bit_identical(built, tmp_path):
         default, st1 = _render_env_process(name, {"FRT_JIT_MIN_PAIRS": str(1 << 18)}, tmp_path / "b.npy", **kw)
         assert st0[0] == 1 and st1[0] == 1 and st0[1] > 0
         assert np.array_equal(stages, default), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_direct_64_4x4", "patterns_160x80", "teapot_low_100", "nave_120x150_4x4",
+                                  "checkered_torus_120", "reflect_refract_test_150", "bounding_boxes_100x125_4x4",
+                                  "area_light_test_100", "checkered_sphere_dof_100", "cornell_gi_24",
+                                  "cornell_shipped_48_4x4"])
+def test_goldens_under_the_production_default(built, name, tmp_path):
+    """The test session walks every level through the beam stages (conftest: FRT_JIT_MIN_PAIRS=0); the shipped default
+    (unset: levels under 2^18 (node, part) pairs walk their rays one by one, i.e. every level of these small scenes)
+    renders one golden per feature group — CSG cornell, patterns, meshes (OBJ, OBJ+MTL textured, the BVH stand-in),
+    torus, refraction, area light, thin-lens aperture, GI, the shipped multi-row light — in a process of its own:
+    deterministic goldens within 1e-4 of the reference with its PPM bytes, and every scene bit-identical to the
+    session's setting."""
+    import hashlib
+    from conftest import golden_index, load_golden_canvas
+    from fast_ray_tracer_amd.runtime import encode_ppm
+    default, st = _render_env_process(name, {"FRT_JIT_MIN_PAIRS": None}, tmp_path / "d.npy")
+    stages, _ = _render_env_process(name, {"FRT_JIT_MIN_PAIRS": "0"}, tmp_path / "s.npy")
+    assert np.array_equal(default, stages), name
+    e = golden_index()[name]
+    if not e.get("stochastic"):
+        img = default[:, :, :3]
+        assert np.abs(img - load_golden_canvas(name)).max() <= 1e-4
+        assert hashlib.sha256(encode_ppm(img)).hexdigest() == e["ppm_sha256"]
