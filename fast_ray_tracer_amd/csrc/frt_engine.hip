@@ -589,17 +589,20 @@ __device__ __forceinline__ void camera_eyev(const DevScene& S, const Batch& B, i
 // A, D, S triples of path node i into out (out[4k + c]: term k, channel c)
 // (lds_row: k_shade_lit's per-wave LDS staging of a multi-row light's row, kLdsPoints points; nullptr elsewhere)
 constexpr int kLdsPoints = 128;
+// (c0 >= 0: the unshadowed count of a scene's one light, staged by the caller; counts[i] is then not read)
 __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, const NodeRec& nr, int64_t i,
-                                           const int32_t* __restrict__ counts, double* out, double* lds_row = nullptr) {
+                                           const int32_t* __restrict__ counts, double* out, double* lds_row = nullptr,
+                                           int32_t c0 = -1) {
     double sA[3] = {0, 0, 0}, sD[3] = {0, 0, 0}, sS[3] = {0, 0, 0};
     if (S.cfg.include_direct) {
         for (int li = 0; li < S.num_lights; ++li) {
             const frt_light& L = S.lights[li];
+            const int32_t cnt = c0 >= 0 ? c0 : counts[i * S.num_lights + li];
             double inten;
             if (L.type == FRT_AREA_LIGHT || L.type == FRT_CIRCLE_LIGHT) {
-                inten = (double)counts[i * S.num_lights + li] / (double)L.num_samples;  // light.c:229-242
+                inten = (double)cnt / (double)L.num_samples;  // light.c:229-242
             } else {
-                inten = counts[i * S.num_lights + li] ? 1.0 : 0.0;  // light.c:245-251
+                inten = cnt ? 1.0 : 0.0;  // light.c:245-251
             }
             double amb[3], cA[3] = {0, 0, 0}, cD[3] = {0, 0, 0}, cS[3] = {0, 0, 0};
             for (int k = 0; k < 3; ++k) amb[k] = nr.Ka[k] * L.intensity[k];
@@ -919,6 +922,56 @@ __global__ void __launch_bounds__(kBlock) k_lit_rows(DevScene S, Batch B, const 
     nodes[m] = i;
 }
 
+// The multi-row light's shading in row order without scattered record traffic (FRT_SHADE_STAGE, default 1; scenes
+// without GI): in row order every lane's node is a random one, so its ~10 record words (NodeCols columns, ShadowHead,
+// counts) were ~10 scattered lines per node and its 9 colour-column stores 9 partial lines (profiles/
+// r05_pmc_k_shade_lit_shipped.json: 7.5 GB fetched, 5.1 GB written per launch for 0.8 GB of triples). k_lit_stage
+// reads the records in list order (the list is in node order within each wave: near-coalesced) and writes what the
+// shading reads as one 96-byte record per listed node (LitStage), indexed by the list position m0 the sort carries as
+// its value; k_shade_lit<true> then reads one record per lane and writes its triple as 72 contiguous bytes at its
+// sorted position m (the wave's 64 triples one 4.6 KB run), with the node's spos[i] = m; k_combine finds the triple
+// through spos. Each lane still computes its own node's result (bit-identical to list order).
+struct LitStage {
+    double over_point[3], normalv[3], eyev[3];
+    uint64_t key;
+    int32_t material, flags;
+    uint32_t node;
+    int32_t c0;  // the one light's unshadowed count (-1: several lights, read from counts)
+};
+static_assert(sizeof(LitStage) == 96, "LitStage layout");
+
+__global__ void __launch_bounds__(kBlock) k_lit_stage(DevScene S, Batch B, NodeCols rec, const int32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ lit, const unsigned* __restrict__ lcount,
+                                                      uint32_t segcap, int sort_light, uint32_t* __restrict__ rows,
+                                                      uint32_t* __restrict__ vals, LitStage* __restrict__ stage) {
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned total = lit_total(lcount);
+    if (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) >= total) return;  // (whole waves)
+    const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
+    if (m >= total) return;
+    const uint32_t i = lit[slot];
+    NodeRec nr = rec.load(i, S.materials);
+    if (rec.eye_cam) camera_eyev(S, B, i, nr.eyev);
+    LitStage r;
+    for (int k = 0; k < 3; ++k) {
+        r.over_point[k] = nr.over_point[k];
+        r.normalv[k] = nr.normalv[k];
+        r.eyev[k] = nr.eyev[k];
+    }
+    r.key = nr.key;
+    r.material = nr.material;
+    r.flags = nr.flags;
+    r.node = i;
+    r.c0 = S.num_lights == 1 ? counts[i] : -1;
+    uint64_t w[12];
+    __builtin_memcpy(w, &r, sizeof(r));
+    uint64_t* dst = (uint64_t*)(stage + m);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) dst[k] = w[k];
+    rows[m] = (uint32_t)light_row(S.lights[sort_light], B.seed, nr.key, sort_light, 1);
+    vals[m] = m;
+}
+
 // the listed nodes (k_shade); one lane each, the grid sized for every node of the level (4 waves per SIMD asked
 // of the compiler: 128 VGPRs with a few spilled outside the light-point loop, 16.5 -> 15.9 ms per headline
 // frame over its own 3)
@@ -931,7 +984,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
                                                       const int32_t* __restrict__ counts, Cols<Tri9> surface,
                                                       const uint32_t* __restrict__ lit,
                                                       const unsigned* __restrict__ lcount, uint32_t segcap,
-                                                      const uint32_t* __restrict__ flat) {
+                                                      const uint32_t* __restrict__ flat,
+                                                      const LitStage* __restrict__ stage, uint32_t* __restrict__ spos) {
     const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
     // the listed total: every lane reads one segment's count (uniform per wave)
     const int lane = threadIdx.x & 63;
@@ -945,16 +999,58 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     const unsigned total = __shfl(incl, 63, 64);
     if (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) >= total) return;  // (whole waves)
     int64_t i = 0;
-    if (flat != nullptr) {  // (the list in row order, k_lit_scatter)
+    NodeRec nr{};
+    int32_t c0 = -1;
+    const bool staged = kRows && stage != nullptr;  // (the staged records in row order, k_lit_stage)
+    if (staged) {
         if (m >= total) return;
-        i = (int64_t)flat[m];
+        const uint64_t* src = (const uint64_t*)(stage + flat[m]);
+        uint64_t w[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) w[k] = src[k];
+        LitStage r;
+        __builtin_memcpy(&r, w, sizeof(r));
+        for (int k = 0; k < 3; ++k) {
+            nr.over_point[k] = r.over_point[k];
+            nr.normalv[k] = r.normalv[k];
+            nr.eyev[k] = r.eyev[k];
+        }
+        nr.key = r.key;
+        nr.material = r.material;
+        nr.flags = r.flags;
+        c0 = r.c0;
+        i = (int64_t)r.node;
     } else {
-        const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
-        if (m >= total) return;
-        i = (int64_t)lit[slot];
+        if (flat != nullptr) {  // (the list in row order)
+            if (m >= total) return;
+            i = (int64_t)flat[m];
+        } else {
+            const size_t slot = jit::mix_slot(m < total ? m : 0u, lcount, segcap);
+            if (m >= total) return;
+            i = (int64_t)lit[slot];
+        }
+        nr = rec.load(i, S.materials);
+        if (rec.eye_cam) camera_eyev(S, B, i, nr.eyev);
     }
-    NodeRec nr = rec.load(i, S.materials);
-    if (rec.eye_cam) camera_eyev(S, B, i, nr.eyev);
+    if (staged) {  // (the colours: a pattern node's own, or its material's)
+        if (nr.flags & kOwnColors) {
+            const NodeColors o = rec.col.load(i);
+            for (int k = 0; k < 3; ++k) {
+                nr.Ka[k] = o.Ka[k];
+                nr.Kd[k] = o.Kd[k];
+                nr.Ks[k] = o.Ks[k];
+            }
+            nr.Ns = o.Ns;
+        } else {
+            const frt_material& M = S.materials[nr.material];
+            for (int k = 0; k < 3; ++k) {
+                nr.Ka[k] = M.Ka[k];
+                nr.Kd[k] = M.Kd[k];
+                nr.Ks[k] = M.Ks[k];
+            }
+            nr.Ns = M.Ns;
+        }
+    }
     double out[12];
 // FRT_SHADE_LDS_ROWS=1: a wave's shared row staged through LDS (A/B runs). 0 (default): read through the scalar
 // cache like the single-row light's points, 14.2 -> 13.1 ms per shipped frame (profiles/r05_ab_shade_scalar_rows.txt)
@@ -963,25 +1059,50 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
 #endif
     if (kRows && FRT_SHADE_LDS_ROWS) {
         __shared__ double lds_rows[kBlock / 64][3 * kLdsPoints];  // (a multi-row light's row per wave, 3 KB)
-        shade_node(S, B, nr, i, counts, out, lds_rows[threadIdx.x >> 6]);
+        shade_node(S, B, nr, i, counts, out, lds_rows[threadIdx.x >> 6], c0);
     } else {
-        shade_node(S, B, nr, i, counts, out);
+        shade_node(S, B, nr, i, counts, out, nullptr, c0);
+    }
+    if (staged) {
+        uint64_t* dst = surface.w + (size_t)9 * m;  // (the level's surface memory as 9-word records, sorted order)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            dst[k] = (uint64_t)__double_as_longlong(out[k]);
+            dst[3 + k] = (uint64_t)__double_as_longlong(out[4 + k]);
+            dst[6 + k] = (uint64_t)__double_as_longlong(out[8 + k]);
+        }
+        spos[i] = m;
+        return;
     }
     tri_store(surface, i, out);
 }
 
 // bottom-up combine of one node (shade_hit's specular block, renderer.c:773-822): its A, D, S triples into col
 // (counts != nullptr: the surface triples of nodes without light-point work were not written, k_shade<true>)
+// (spos != nullptr: the level's lit nodes were shaded in row order from staged records, k_lit_stage; a lit node's
+// triple is the 9-word record spos[i] of the surface memory)
 __device__ __forceinline__ void combine_node(const DevScene& S, const int32_t* __restrict__ counts,
                                              const NodeRec& nr, int64_t i, Cols<Tri9> surface, Cols<Tri9> child,
                                              const frt_material* __restrict__ mats, int32_t include_specular,
-                                             double* col) {
+                                             double* col, const uint32_t* __restrict__ spos = nullptr) {
     if (nr.material < 0) {
         for (int k = 0; k < 12; ++k) col[k] = 0.0;
         return;
     }
-    if (counts != nullptr && !shade_heavy(S, counts, i)) ambient_node(S, nr, col);
-    else tri_load(surface, i, col);
+    if (counts != nullptr && !shade_heavy(S, counts, i)) {
+        ambient_node(S, nr, col);
+    } else if (spos != nullptr) {
+        const uint64_t* src = surface.w + (size_t)9 * spos[i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            col[k] = __longlong_as_double((long long)src[k]);
+            col[4 + k] = __longlong_as_double((long long)src[3 + k]);
+            col[8 + k] = __longlong_as_double((long long)src[6 + k]);
+        }
+        col[3] = col[7] = col[11] = 0.0;
+    } else {
+        tri_load(surface, i, col);
+    }
     if (include_specular) {
         const frt_material& M = mats[nr.material];
         // reflected / refracted_color from the children's slots; a child that was not traced
@@ -1022,12 +1143,13 @@ __device__ __forceinline__ void combine_node(const DevScene& S, const int32_t* _
 __global__ void __launch_bounds__(kBlock) k_combine(DevScene S, const int32_t* __restrict__ counts, NodeCols rec,
                                                     int64_t n, Cols<Tri9> surface, Cols<Tri9> child,
                                                     Cols<Tri9> parent_child, Cols<Tri9> sample_out, int32_t spp,
-                                                    const frt_material* __restrict__ mats, int32_t include_specular) {
+                                                    const frt_material* __restrict__ mats, int32_t include_specular,
+                                                    const uint32_t* __restrict__ spos) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const NodeRec nr = rec.load(i, mats);
     double col[12];
-    combine_node(S, counts, nr, i, surface, child, mats, include_specular, col);
+    combine_node(S, counts, nr, i, surface, child, mats, include_specular, col, spos);
     if (nr.parent >= 0) {
         tri_store(parent_child, 2 * (int64_t)nr.parent + nr.slot, col);  // a missed child writes its zeros
     } else {
@@ -1044,7 +1166,8 @@ __global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(DevScene S, cons
                                                                 NodeCols rec, int64_t n, Cols<Tri9> surface,
                                                                 Cols<Tri9> child, int32_t spp, int32_t ppb,
                                                                 int64_t npix, const frt_material* __restrict__ mats,
-                                                                int32_t include_specular, double* __restrict__ out) {
+                                                                int32_t include_specular, double* __restrict__ out,
+                                                                const uint32_t* __restrict__ spos) {
     // (each pixel's column sum goes back into the first slot of the run it was summed from: only the thread that
     // summed a run reads it, and the block's LDS stays at 18.5 KB, so six blocks fit a CU instead of four)
 #ifndef FRT_RESOLVE_INPLACE
@@ -1060,7 +1183,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_combine_resolve(DevScene S, cons
     if (t < ppb * spp && i < n) {
         const NodeRec nr = rec.load(i, mats);
         double col[12];
-        combine_node(S, counts, nr, i, surface, child, mats, include_specular, col);
+        combine_node(S, counts, nr, i, surface, child, mats, include_specular, col, spos);
 #pragma unroll
         for (int f = 0; f < 9; ++f) stage[f][t] = col[(f / 3) * 4 + f % 3];
     }
@@ -1833,10 +1956,13 @@ struct frt_scene_handle {
     // the lit list in row order (k_shade -> k_lit_rows -> radix sort) for a multi-row light: the listed nodes' rows
     // (keys, and the sort's alternate buffer), the ordered list (and the unsorted values)
     int sort_light = -1;               // the first light with more than one cache row (FRT_SHADE_SORT=0: none)
+    bool shade_stage = false;          // its shading from staged records (k_lit_stage, FRT_SHADE_STAGE)
     uint32_t* lit_row = nullptr;
     int64_t lit_row_cap = 0;
     uint32_t* lit_flat = nullptr;
     int64_t lit_flat_cap = 0;
+    frt::LitStage* lit_stage = nullptr;  // (k_lit_stage's records, FRT_SHADE_STAGE)
+    int64_t lit_stage_cap = 0;
     unsigned char* scan_tmp = nullptr;  // (the device sort's temporary storage)
     int64_t scan_tmp_cap = 0;
     unsigned* shade_lcount = nullptr;
@@ -1853,6 +1979,8 @@ struct frt_scene_handle {
         int64_t* qprefix = nullptr;                     // queue segments of this level (frt_shadow.hpp)
         std::vector<int64_t> hprefix = std::vector<int64_t>(frt::kQueueSegs + 1, 0);
         int32_t* counts = nullptr;
+        uint32_t* spos = nullptr;  // (lit nodes shaded from staged records: a node's sorted position, k_shade_lit)
+        bool staged = false;       // this batch's shading of the level went through k_lit_stage
         int64_t cap = 0;
     };
     std::vector<Level> levels;
@@ -2913,6 +3041,10 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         h->sort_light = -1;
         for (int l = 0; l < sc->num_lights && h->sort_light < 0 && !(e && std::atoi(e) == 0); ++l)
             if (sc->lights[l].rows > 1 && sc->lights[l].num_samples > 0) h->sort_light = l;
+        // the row-ordered shading from staged records (k_lit_stage); FRT_SHADE_STAGE=0: the node records read in row
+        // order, as round 5 did (A/B runs)
+        const char* se = std::getenv("FRT_SHADE_STAGE");
+        h->shade_stage = h->sort_light >= 0 && !(se && std::atoi(se) == 0);
     }
     // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
     // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L
@@ -3033,6 +3165,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(L.surface.w));
         hip_ignore(hipFree(L.child.w));
         hip_ignore(hipFree(L.counts));
+        hip_ignore(hipFree(L.spos));
         hip_ignore(hipFree(L.qprefix));
     }
     hip_ignore(hipFree(h->hits));
@@ -3063,6 +3196,7 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->shade_lcount));
     hip_ignore(hipFree(h->lit_row));
     hip_ignore(hipFree(h->lit_flat));
+    hip_ignore(hipFree(h->lit_stage));
     hip_ignore(hipFree(h->scan_tmp));
     hip_ignore(hipFree(h->mixed));
     hip_ignore(hipFree(h->tlist));
@@ -3090,6 +3224,8 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     hip_ignore(hipFree(L.surface.w));
     hip_ignore(hipFree(L.child.w));
     hip_ignore(hipFree(L.counts));
+    hip_ignore(hipFree(L.spos));
+    L.spos = nullptr;
     L.rec = {};
     L.q = nullptr;
     L.surface = {};
@@ -3113,6 +3249,7 @@ static int ensure_level(frt_scene_handle* h, size_t d, int64_t need) {
     L.child.cap = 2 * nc;
     if (!L.qprefix) FRT_HIP(hipMalloc((void**)&L.qprefix, (frt::kQueueSegs + 1) * sizeof(int64_t)));
     FRT_HIP(hipMalloc((void**)&L.counts, nc * std::max(1, h->S.num_lights) * sizeof(int32_t)));
+    if (h->shade_stage) FRT_HIP(hipMalloc((void**)&L.spos, nc * sizeof(uint32_t)));
     L.cap = nc;
     return 0;
 }
@@ -4506,10 +4643,14 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 const int nrows = sorted ? std::max(1, h->host_lights[(size_t)h->sort_light].rows) : 0;
                 int row_bits = 1;
                 while (row_bits < 32 && (1ll << row_bits) < nrows) ++row_bits;
+                // (the staged records: without GI, whose kernels read and write the surface columns by node)
+                const bool staged = sorted && shade_lazy(h) && L.spos != nullptr && h->shade_stage;
+                L.staged = staged;
                 if (sorted) {
                     const int64_t lcap = (int64_t)segcap * kShadeSegs;
                     if (grow(&h->lit_row, h->lit_row_cap, 2 * lcap) || grow(&h->lit_flat, h->lit_flat_cap, 2 * lcap))
                         return -1;
+                    if (staged && grow(&h->lit_stage, h->lit_stage_cap, lcap)) return -1;
                 }
                 if (shade_lazy(h))
                     hipLaunchKernelGGL(k_shade<true>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec, n,
@@ -4521,8 +4662,13 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                     KTimer ts(h, st, 16);  // (k_lit_rows + the radix sort, sub_ms["k_lit_sort"])
                     const int64_t lcap = (int64_t)segcap * kShadeSegs;
                     uint32_t *keys = h->lit_row, *keys2 = h->lit_row + lcap, *vals = h->lit_flat + lcap;
-                    hipLaunchKernelGGL(k_lit_rows, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.head,
-                                       h->shade_lit, h->shade_lcount, segcap, h->sort_light, keys, vals);
+                    if (staged)
+                        hipLaunchKernelGGL(k_lit_stage, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.rec,
+                                           L.counts, h->shade_lit, h->shade_lcount, segcap, h->sort_light, keys, vals,
+                                           h->lit_stage);
+                    else
+                        hipLaunchKernelGGL(k_lit_rows, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S, B, L.head,
+                                           h->shade_lit, h->shade_lcount, segcap, h->sort_light, keys, vals);
                     // (the listed count on the host: the sort's size)
                     auto& lc = h->host_lcount;
                     FRT_HIP(hipMemcpyAsync(lc.data(), h->shade_lcount, lc.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
@@ -4555,7 +4701,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                     hipLaunchKernelGGL(sorted ? k_shade_lit<true> : k_shade_lit<false>, dim3(grid_for(n, FRT_SHADE_LIT_BLOCK)),
                                        dim3(FRT_SHADE_LIT_BLOCK), 0,
                                        h->stream, h->S, B, L.rec, L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap,
-                                       sorted ? (const uint32_t*)h->lit_flat : nullptr);
+                                       sorted ? (const uint32_t*)h->lit_flat : nullptr,
+                                       staged ? (const frt::LitStage*)h->lit_stage : nullptr, L.spos);
                 }
                 FRT_HIP(hipGetLastError());
             }
@@ -4603,7 +4750,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 const int32_t ppb = kFuseBlock / spp;
                 hipLaunchKernelGGL(k_combine_resolve, dim3((unsigned)((bp + ppb - 1) / ppb)), dim3(kFuseBlock), 0, h->stream,
                                    h->S, lazy ? h->levels[0].counts : nullptr, h->levels[0].rec, n, h->levels[0].surface, h->levels[0].child, spp, ppb, bp,
-                                   h->S.materials, h->S.cfg.include_specular, dev_out + 4 * p0);
+                                   h->S.materials, h->S.cfg.include_specular, dev_out + 4 * p0,
+                                   h->levels[0].staged ? (const uint32_t*)h->levels[0].spos : nullptr);
                 FRT_HIP(hipGetLastError());
                 continue;
             }
@@ -4612,7 +4760,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             hipLaunchKernelGGL(k_combine, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, h->S,
                                lazy ? h->levels[d].counts : nullptr, h->levels[d].rec, n,
                                h->levels[d].surface, h->levels[d].child, parent_child, h->sample_col, spp,
-                               h->S.materials, h->S.cfg.include_specular);
+                               h->S.materials, h->S.cfg.include_specular,
+                               h->levels[d].staged ? (const uint32_t*)h->levels[d].spos : nullptr);
             FRT_HIP(hipGetLastError());
         }
         if (!fuse) {

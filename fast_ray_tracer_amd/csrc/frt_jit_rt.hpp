@@ -338,6 +338,27 @@ __device__ __forceinline__ void count_part(const DevScene& S, const Lane32& L, b
     }
 }
 
+// the lit lanes of each run of consecutive valid lanes with the same (node, light) (the per-ray kernel's node-major
+// lanes: a node's samples of several list entries side by side), one atomic per run by its first lane (all lanes of
+// the wave)
+__device__ __forceinline__ void count_runs(const DevScene& S, const Lane32& L, bool lit, int32_t* counts) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lits = __ballot(lit), valid = __ballot(L.valid);
+    const uint32_t key = L.node * (uint32_t)S.num_lights + (uint32_t)L.light;
+    const uint32_t prev = __shfl_up(key, 1, 64);
+    const bool prev_valid = lane > 0 && ((valid >> (lane - 1)) & 1ull);
+    const bool head = L.valid && (!prev_valid || prev != key);
+    const unsigned long long heads = __ballot(head);
+    if (head) {
+        const unsigned long long after = lane == 63 ? 0ull : (~0ull << (lane + 1));
+        const unsigned long long stops = (heads | ~valid) & after;
+        const int next = stops ? __ffsll((long long)stops) - 1 : 64;
+        const unsigned long long run = (next >= 64 ? ~0ull : ((1ull << next) - 1ull)) & (~0ull << lane);
+        const int c = __popcll(lits & run);
+        if (c) atomicAdd(counts + key, c);
+    }
+}
+
 // (all lanes of the wave) mixed index m -> its slot in the segmented list
 __device__ __forceinline__ size_t mix_slot(uint32_t m, const unsigned* __restrict__ mcount, uint32_t segcap) {
     const int lane = threadIdx.x & 63;

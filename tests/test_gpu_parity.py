@@ -419,7 +419,7 @@ def test_math_core_sequences_bit_identical(built):
                                        ("cornell_shipped_1920x1080_8x8", (520, 528))])
 def test_row_sorted_shading_equals_list_order(built, name, rows):
     """With a multi-row light (the shipped 65 535-row cache) the lit nodes are shaded in the order of the light row
-    their shading draw picks (k_lit_scan / k_lit_scatter), so a wave mostly shares one row and reads it through the
+    their shading draw picks (k_lit_stage / k_lit_rows and a radix sort), so a wave mostly shares one row and reads it through the
     scalar cache. Each lane still shades its own node, so the canvas equals the one in list order (FRT_SHADE_SORT=0)
     bit for bit: the shipped direct configuration, a GI one and a band of the shipped 1920x1080x64 frame."""
     kw = {} if rows is None else {"row_begin": rows[0], "row_end": rows[1]}
@@ -427,6 +427,10 @@ def test_row_sorted_shading_equals_list_order(built, name, rows):
     plain = _render_env(name, {"FRT_SHADE_SORT": "0"}, **kw)
     assert np.isfinite(sorted_).all() and sorted_[:, :, :3].max() > 0
     assert np.array_equal(sorted_, plain)
+    # without GI the row-ordered shading reads staged records and writes its triples in row order (k_lit_stage,
+    # combine through spos); FRT_SHADE_STAGE=0 reads the node records in row order as round 5 did
+    unstaged = _render_env(name, {"FRT_SHADE_SORT": "1", "FRT_SHADE_STAGE": "0"}, **kw)
+    assert np.array_equal(unstaged, plain)
 
 
 def test_render_multi_keeps_handles_between_calls(built):

@@ -160,7 +160,9 @@ def test_tile_and_sub_part_kernels_equal_generic_walk(built, name, tmp_path):
                              {"FRT_JIT_TILE": "8", "FRT_JIT_SUB": "8", "FRT_JIT_MAX_PAIRS": "4099"},
                              # the sub-tile (sub-part) stage's list walked ray by ray without the node pair kernel
                              {"FRT_JIT_NODE_BEAM": "0"}, {"FRT_JIT_NODE_BEAM": "0", "FRT_JIT_SUBTILE": "0"},
-                             {"FRT_JIT_NODE_BEAM": "1"}, {"FRT_JIT_SUBTILE_DEEP": "0"})):
+                             {"FRT_JIT_NODE_BEAM": "1"}, {"FRT_JIT_SUBTILE_DEEP": "0"},
+                             # node-major lanes over the stage's list (groups of 4 / 64 entries; a last group short)
+                             {"FRT_JIT_NODE_MAJOR": "4"}, {"FRT_JIT_NODE_MAJOR": "64", "FRT_JIT_SUBTILE": "0"})):
         img, st = _render_env_process(name, env, tmp_path / ("j%d.npy" % i))
         assert st[0] == 1 and st[1] > 0, (env, st)
         if env.get("FRT_JIT_SUB") != "0":
@@ -202,13 +204,14 @@ def test_tile_kernels_on_shipped_multi_row_light(built, tmp_path):
     (u, v) of every row in light cell (u, v)), frt_jit_beam_list against the node's own row. At a fixed seed, row bands
     of the shipped 1920x1080x64 frame through the whole hierarchy, through the node pair kernel alone
     (FRT_JIT_TILE=0) and through the generic walk are bit-identical, and the tile stages ran — with the sub-tile stage's
-    list walked ray by ray (the default for multi-row lights), through frt_jit_beam_list (FRT_JIT_NODE_BEAM=1) and
-    without the sub-tile stage."""
+    list walked ray by ray (the default for multi-row lights), through frt_jit_beam_list (FRT_JIT_NODE_BEAM=1),
+    without the sub-tile stage, and with the per-ray kernel's lanes entry-major or node-major (FRT_JIT_NODE_MAJOR)."""
     for rows in ((300, 306), (700, 706)):
         kw = {"row_begin": rows[0], "row_end": rows[1], "seed": 0x5EED}
         ref, st = _render_env_process("cornell_shipped_1920x1080_8x8", {"FRT_JIT": "0"}, tmp_path / "g.npy", **kw)
         assert st[0] == 0
-        for i, env in enumerate(({}, {"FRT_JIT_NODE_BEAM": "1"}, {"FRT_JIT_SUBTILE": "0"})):
+        for i, env in enumerate(({}, {"FRT_JIT_NODE_BEAM": "1"}, {"FRT_JIT_SUBTILE": "0"}, {"FRT_JIT_NODE_MAJOR": "1"},
+                                 {"FRT_JIT_NODE_MAJOR": "8"}, {"FRT_JIT_NODE_MAJOR": "64"})):
             img, st = _render_env_process("cornell_shipped_1920x1080_8x8", env, tmp_path / ("t%d.npy" % i), **kw)
             assert st[0] == 1 and st[1] > 0 and st[2] > 0, (env, st)
             assert np.array_equal(img, ref), (rows, env)

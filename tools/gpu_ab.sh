@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: headline-style A/B of engine knobs on one scene: tools/gpu_r05_ab.sh <scene> <label> "<ENV=..>" ["<ENV=..>" ...]
+# headline-style A/B of engine knobs on one scene: tools/gpu_ab.sh <scene> <label> "<ENV=..>" ["<ENV=..>" ...]
 # (each variant one bench.py process, steps 5, the stats frame's kernel split; a line per variant in gpurun_out/ab_<label>.txt)
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 5: A/B of device-library builds (variants/<name>.so from tools/build_variant.sh; "base" = the tree's build) on
-# one scene, each through tools/gpu_r05_ab.sh:   tools/gpu_r05_var.sh <scene> <label> base NAME ... [base]
+# A/B of device-library builds (variants/<name>.so from tools/build_variant.sh; "base" = the tree's build) on
+# one scene, each through tools/gpu_ab.sh:   tools/gpu_var.sh <scene> <label> base NAME ... [base]
 set -o pipefail
 sc=$1; label=$2; shift 2
 cp fast_ray_tracer_amd/lib/libfrt_device.so /tmp/frt_base.so
@@ -8,7 +8,7 @@ cp fast_ray_tracer_amd/lib/libfrt_device.so /tmp/frt_base.so
 rc=0
 for lib in "$@"; do
   if [ "$lib" = base ]; then cp /tmp/frt_base.so fast_ray_tracer_amd/lib/libfrt_device.so; else cp variants/$lib.so fast_ray_tracer_amd/lib/libfrt_device.so; fi
-  bash tools/gpu_r05_ab.sh $sc ${label}_$lib "FRT_LIB=$lib" || { rc=1; break; }
+  bash tools/gpu_ab.sh $sc ${label}_$lib "FRT_LIB=$lib" || { rc=1; break; }
   cat gpurun_out/ab_${label}_$lib.txt >> gpurun_out/ab_${label}_all.txt
 done
 cp /tmp/frt_base.so fast_ray_tracer_amd/lib/libfrt_device.so
