@@ -1002,6 +1002,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     NodeRec nr{};
     int32_t c0 = -1;
     const bool staged = kRows && stage != nullptr;  // (the staged records in row order, k_lit_stage)
+    const bool sorted_out = kRows && spos != nullptr;  // (the triples in row order, found through spos)
     if (staged) {
         if (m >= total) return;
         const uint64_t* src = (const uint64_t*)(stage + flat[m]);
@@ -1063,7 +1064,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT
     } else {
         shade_node(S, B, nr, i, counts, out, nullptr, c0);
     }
-    if (staged) {
+    if (sorted_out) {
         uint64_t* dst = surface.w + (size_t)9 * m;  // (the level's surface memory as 9-word records, sorted order)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -1956,7 +1957,7 @@ struct frt_scene_handle {
     // the lit list in row order (k_shade -> k_lit_rows -> radix sort) for a multi-row light: the listed nodes' rows
     // (keys, and the sort's alternate buffer), the ordered list (and the unsorted values)
     int sort_light = -1;               // the first light with more than one cache row (FRT_SHADE_SORT=0: none)
-    bool shade_stage = false;          // its shading from staged records (k_lit_stage, FRT_SHADE_STAGE)
+    int shade_stage = 0;               // its shading from staged records / into row order (FRT_SHADE_STAGE)
     uint32_t* lit_row = nullptr;
     int64_t lit_row_cap = 0;
     uint32_t* lit_flat = nullptr;
@@ -3041,10 +3042,10 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         h->sort_light = -1;
         for (int l = 0; l < sc->num_lights && h->sort_light < 0 && !(e && std::atoi(e) == 0); ++l)
             if (sc->lights[l].rows > 1 && sc->lights[l].num_samples > 0) h->sort_light = l;
-        // the row-ordered shading from staged records (k_lit_stage); FRT_SHADE_STAGE=0: the node records read in row
-        // order, as round 5 did (A/B runs)
+        // the row-ordered shading: 1 from staged records (k_lit_stage) with its triples in row order (spos), 2 the node
+        // records read in row order with the triples in row order, 0 both by node as round 5 did (FRT_SHADE_STAGE)
         const char* se = std::getenv("FRT_SHADE_STAGE");
-        h->shade_stage = h->sort_light >= 0 && !(se && std::atoi(se) == 0);
+        h->shade_stage = h->sort_light >= 0 ? (se ? std::atoi(se) : 1) : 0;
     }
     // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
     // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L
@@ -4644,8 +4645,9 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 int row_bits = 1;
                 while (row_bits < 32 && (1ll << row_bits) < nrows) ++row_bits;
                 // (the staged records: without GI, whose kernels read and write the surface columns by node)
-                const bool staged = sorted && shade_lazy(h) && L.spos != nullptr && h->shade_stage;
-                L.staged = staged;
+                const bool sorted_out = sorted && shade_lazy(h) && L.spos != nullptr && h->shade_stage > 0;
+                const bool staged = sorted_out && h->shade_stage == 1;
+                L.staged = sorted_out;
                 if (sorted) {
                     const int64_t lcap = (int64_t)segcap * kShadeSegs;
                     if (grow(&h->lit_row, h->lit_row_cap, 2 * lcap) || grow(&h->lit_flat, h->lit_flat_cap, 2 * lcap))
@@ -4702,7 +4704,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                                        dim3(FRT_SHADE_LIT_BLOCK), 0,
                                        h->stream, h->S, B, L.rec, L.counts, L.surface, h->shade_lit, h->shade_lcount, segcap,
                                        sorted ? (const uint32_t*)h->lit_flat : nullptr,
-                                       staged ? (const frt::LitStage*)h->lit_stage : nullptr, L.spos);
+                                       staged ? (const frt::LitStage*)h->lit_stage : nullptr,
+                                       sorted_out ? L.spos : nullptr);
                 }
                 FRT_HIP(hipGetLastError());
             }

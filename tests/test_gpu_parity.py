@@ -429,8 +429,9 @@ def test_row_sorted_shading_equals_list_order(built, name, rows):
     assert np.array_equal(sorted_, plain)
     # without GI the row-ordered shading reads staged records and writes its triples in row order (k_lit_stage,
     # combine through spos); FRT_SHADE_STAGE=0 reads the node records in row order as round 5 did
-    unstaged = _render_env(name, {"FRT_SHADE_SORT": "1", "FRT_SHADE_STAGE": "0"}, **kw)
-    assert np.array_equal(unstaged, plain)
+    for mode in ("0", "2"):  # (2: the node records read in row order, the triples still written in row order)
+        other = _render_env(name, {"FRT_SHADE_SORT": "1", "FRT_SHADE_STAGE": mode}, **kw)
+        assert np.array_equal(other, plain), mode
 
 
 def test_render_multi_keeps_handles_between_calls(built):
