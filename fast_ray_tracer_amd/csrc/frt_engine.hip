@@ -922,8 +922,8 @@ __global__ void __launch_bounds__(kBlock) k_lit_rows(DevScene S, Batch B, const 
     nodes[m] = i;
 }
 
-// The multi-row light's shading in row order without scattered record traffic (FRT_SHADE_STAGE, default 1; scenes
-// without GI): in row order every lane's node is a random one, so its ~10 record words (NodeCols columns, ShadowHead,
+// The multi-row light's shading in row order without scattered record traffic (FRT_SHADE_STAGE=1; scenes without
+// GI; the default, 2, keeps only the triples' part): in row order every lane's node is a random one, so its ~10 record words (NodeCols columns, ShadowHead,
 // counts) were ~10 scattered lines per node and its 9 colour-column stores 9 partial lines (profiles/
 // r05_pmc_k_shade_lit_shipped.json: 7.5 GB fetched, 5.1 GB written per launch for 0.8 GB of triples). k_lit_stage
 // reads the records in list order (the list is in node order within each wave: near-coalesced) and writes what the
@@ -3042,10 +3042,11 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         h->sort_light = -1;
         for (int l = 0; l < sc->num_lights && h->sort_light < 0 && !(e && std::atoi(e) == 0); ++l)
             if (sc->lights[l].rows > 1 && sc->lights[l].num_samples > 0) h->sort_light = l;
-        // the row-ordered shading: 1 from staged records (k_lit_stage) with its triples in row order (spos), 2 the node
-        // records read in row order with the triples in row order, 0 both by node as round 5 did (FRT_SHADE_STAGE)
+        // the row-ordered shading (FRT_SHADE_STAGE): 2 (default) the node records read in row order, the triples
+        // written in row order (spos); 1 also the records staged in list order first (k_lit_stage); 0 both by node, as
+        // round 5 did. Shipped frame: shade 14.2 / 13.1 / 12.9 ms for 0 / 1 / 2 (profiles/r06_ab_shipped_modes.txt)
         const char* se = std::getenv("FRT_SHADE_STAGE");
-        h->shade_stage = h->sort_light >= 0 ? (se ? std::atoi(se) : 1) : 0;
+        h->shade_stage = h->sort_light >= 0 ? (se ? std::atoi(se) : 2) : 0;
     }
     // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
     // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L

@@ -372,13 +372,17 @@ __device__ __forceinline__ unsigned wave_and(bool v) { return __ballot(!v) == 0u
 // sqrt(x) for x >= 0 within a few ulps (v_rsq_f64 and two Newton steps): the cone filter's weights only
 // scale the sums (which run in another order than the reference's anyway); every decision of the
 // selection uses exact squared distances
+#ifndef FRT_SQRTW_STEPS
+#define FRT_SQRTW_STEPS 2
+#endif
 __device__ __forceinline__ double sqrt_w(double x) {
     const double y = __builtin_amdgcn_rsq(x);
     double s = x * y, h = 0.5 * y;
-    double r = fma(-s, s, x);
-    s = fma(r, h, s);
-    r = fma(-s, s, x);
-    s = fma(r, h, s);
+#pragma unroll
+    for (int k = 0; k < FRT_SQRTW_STEPS; ++k) {
+        const double r = fma(-s, s, x);
+        s = fma(r, h, s);
+    }
     return x > 0.0 ? s : 0.0;
 }
 
