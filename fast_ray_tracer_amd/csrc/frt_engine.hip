@@ -350,7 +350,7 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
     c.n1 = hn12 != nullptr ? hn12[2 * node] : 1.0;
     c.n2 = hn12 != nullptr ? hn12[2 * node + 1] : 1.0;
     PSTAMP(2);
-    wave_count(line + 17, true);  // shaded path nodes
+    if (B.stats) wave_count(line + 17, true);  // shaded path nodes (statistics frames only: an atomic per wave)
     const frt_material& M = S.materials[c.material];
     NodeRec nr;
     for (int k = 0; k < 3; ++k) {
@@ -408,8 +408,10 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
         // slots in this block's segment of the next level's queue
         const unsigned long long at_refl = wave_append(line + B.level + 1, want_refl);
         const unsigned long long at_refr = wave_append(line + B.level + 1, want_refr);
-        wave_count(line + 16, reflect_applies && !want_refl);  // pruned zero-weight rays
-        wave_count(line + 16, refract_applies && !want_refr);
+        if (B.stats) {  // pruned zero-weight rays (statistics frames only)
+            wave_count(line + 16, reflect_applies && !want_refl);
+            wave_count(line + 16, refract_applies && !want_refr);
+        }
         if (want_refl) {
             if ((int64_t)at_refl < B.next_segcap) {
                 QueuedRay qo;
@@ -3454,7 +3456,20 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         const bool beam_on = h->jit_beam_on && n * NP >= min_pairs;
         const bool tiled = beam_on && h->tile > 0 && h->jit_tile && h->jit_list && h->tbox;
         const bool subbed = tiled && h->jit_sub && h->sub > 0 && h->light_psamp2 && h->light_sbox;
-        if (subbed) kMaxPairs = std::min<int64_t>(kMaxPairs, (int64_t)(0xFFFFFFFFull / (uint64_t)h->sub));
+        if (subbed && h->node_beam) {
+            kMaxPairs = std::min<int64_t>(kMaxPairs, (int64_t)(0xFFFFFFFFull / (uint64_t)h->sub));
+        } else if (subbed) {
+            // (the stages' lists hold tile-level entries, ((tile * NP + part) * sub + q) << log2(tile / subtile) +
+            // sub-tile, and node pairs node * NP + part where a level's list goes to the node pair kernel: a level
+            // runs in one range while both fit 32 bits — the headline's level 0, 132.7 M nodes, in one range instead
+            // of four, a quarter of the stage launches and host round trips)
+            int stl = 0;
+            while (h->subtile > 0 && (1 << stl) < h->tile / h->subtile) ++stl;
+            const uint64_t per_tile = ((uint64_t)NP * (uint64_t)h->sub) << stl;
+            const int64_t tiled_max = (int64_t)(0xFFFFFFFFull / per_tile) * h->tile * NP;
+            kMaxPairs = std::min<int64_t>(std::min<int64_t>(tiled_max, (int64_t)0xFFFFFFFFll),
+                                          mp >= 1 && mp < (1ll << 31) ? (int64_t)mp : INT64_MAX);
+        }
         if (n * NP > kMaxPairs) {
             int64_t per = std::max<int64_t>(1, kMaxPairs / NP);
             if (h->tile > 0) per = std::max<int64_t>(h->tile, per / h->tile * h->tile);
@@ -4560,6 +4575,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
         B.row_stride = stride;
         B.seed = P->seed;
         B.spp = spp;
+        B.stats = st != nullptr ? 1 : 0;
         std::vector<int64_t> count(path + 2, 0);
         count[0] = ns;
         // the queue counts (words 0..15) of every counter line

@@ -46,7 +46,7 @@ struct Batch {
     uint64_t seed;
     int32_t spp, level;
     int32_t remaining;     // path_length - level
-    int32_t pad;
+    int32_t stats;         // the frame collects statistics (frt_frame_stats): the diagnostic counters are counted
     const int64_t* qprefix;  // this level's queue segments (kQueueSegs + 1 prefix counts); null: contiguous
     int64_t qsegcap;         // entries per segment of this level's queue
     int64_t next_segcap;     // entries per segment of the next level's queue
