@@ -500,10 +500,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPa
 k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const HitRec* __restrict__ hits,
           const double* __restrict__ hn12,
           NodeCols rec, ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q, unsigned long long* counters,
-          unsigned* err, float* __restrict__ tbox, int tile_log2, float* __restrict__ stbox, int sub_log2) {
+          unsigned* err, float* __restrict__ tbox, int tile_log2, float* __restrict__ stbox, int sub_log2,
+          int32_t* __restrict__ counts) {
     const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double op[3] = {0.0, 0.0, 0.0};
     bool hit = false;
+    // (the level's unshadowed counts start at 0: zeroed here, in the node's own coalesced words, instead of a
+    // memset launch per level)
+    if (node < n && counts != nullptr)
+        for (int l = 0; l < S.num_lights; ++l) counts[node * S.num_lights + l] = 0;
     if (node < n) hit = prepare_node<kPat>(S, B, q, n, hits, hn12, rec, heads, next_q, counters, err, node, op);
     if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2, stbox, sub_log2);
 }
@@ -1940,7 +1945,8 @@ struct frt_scene_handle {
     const float* light_aabb = nullptr; // per light, per cache row: the points' box (binary32, outward)
     uint32_t* mixed = nullptr;         // mixed (node, light) pairs, kMixSegs segments
     int64_t mixed_cap = 0;
-    unsigned* mcount = nullptr;        // the segments' counters (kMixSegs lines of kMixLine words)
+    unsigned* mcount = nullptr;        // the segments' counters (kMixSegs lines of kMixLine words): four regions, one per
+                                       // stage of a shadow pass (tile, sub-part, sub-tile, node pairs), zeroed together
     uint64_t sync_epoch = 0;           // stream_sync calls (the level loop's early counter read-back)
     PinnedBuf<unsigned> host_mcount;
     PinnedBuf<unsigned long long> host_counters;  // (the level's queue counters, read back per level)
@@ -2972,7 +2978,7 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
                     h->light_psamp2 = upload(h, ps2.data(), ps2.size(), rc);
                     h->light_sbox = upload(h, sbox.data(), sbox.size(), rc);
                 }
-                if (rc || hipMalloc((void**)&h->mcount, frt::jit::kMixSegs * frt::jit::kMixLine * sizeof(unsigned)) != hipSuccess) {
+                if (rc || hipMalloc((void**)&h->mcount, 4 * frt::jit::kMixSegs * frt::jit::kMixLine * sizeof(unsigned)) != hipSuccess) {
                     frt_scene_release(h);
                     return fail("frt_scene_upload: light box / pair list allocation failed");
                 }
@@ -3480,6 +3486,12 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
         const int64_t npairs = n * NP;
         uint32_t nn = (uint32_t)n;
         uint32_t segcap = 0;
+        // the stages' list counters, one region each, zeroed by one memset for the pass
+        unsigned* mc_tile = h->mcount;
+        unsigned* mc_sub = h->mcount + kMixSegs * kMixLine;
+        unsigned* mc_subtile = h->mcount + 2 * kMixSegs * kMixLine;
+        unsigned* mc_node = h->mcount + 3 * kMixSegs * kMixLine;
+        if (beam_on) hip_ignore(hipMemsetAsync(h->mcount, 0, 4 * kMixSegs * kMixLine * sizeof(unsigned), h->stream));
         uint64_t total_mixed = 0;
         const uint32_t* direct_in = nullptr;  // (the sub / sub-tile list walked by the per-ray kernel directly)
         uint32_t direct_subq = 0, direct_nodes = 0;
@@ -3504,12 +3516,11 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     launch_shadow(h, B, rec, n, counts, node0);
                     return;
                 }
-                hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
                 const float* tb = h->tbox + 6 * (node0 >> tl);
                 const uint32_t* no_list = nullptr;
                 uint32_t zero = 0;
                 void* targs[] = {&h->S, (void*)&B, (void*)&rec, &ntp, &nn, (void*)&tb, (void*)&no_list, &tseg, &zero, &zero,
-                                 &h->light_aabb, &counts, &h->tlist, &h->mcount, &tsegcap, &h->err, &h->jit_stats,
+                                 &h->light_aabb, &counts, &h->tlist, &mc_tile, &tsegcap, &h->err, &h->jit_stats,
                                  &h->light_psamp2};
                 hipError_t le;
                 {
@@ -3525,7 +3536,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     launch_shadow(h, B, rec, n, counts, node0);
                     return;
                 }
-                if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                if (hipMemcpyAsync(h->host_mcount.data(), mc_tile, h->host_mcount.size() * sizeof(unsigned),
                                    hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                     stream_sync(h) != hipSuccess)
                     return;
@@ -3548,7 +3559,6 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         launch_shadow(h, B, rec, n, counts, node0);
                         return;
                     }
-                    hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
                     hipError_t se = hipSuccess;
                     {
                         KTimer ts(h, h->cur_st, 13);
@@ -3557,7 +3567,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         for (uint64_t b0 = 0; b0 < sblocks && se == hipSuccess; b0 += max_blocks) {
                             uint32_t b0u = (uint32_t)b0;
                             void* sargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&tb, &h->tlist, (void*)&sseg, &b0u,
-                                             &tsegcap, &h->light_sbox, &counts, &h->slist, &h->mcount, (void*)&ssegcap, &h->err,
+                                             &tsegcap, &h->light_sbox, &counts, &h->slist, &mc_sub, (void*)&ssegcap, &h->err,
                                              &h->jit_stats, &h->light_psamp2};
                             se = hipModuleLaunchKernel((hipFunction_t)h->jit_sub, (unsigned)std::min(max_blocks, sblocks - b0), 1, 1,
                                                        frt::kTraceBlock, 1, 1, 0, h->stream, sargs, nullptr);
@@ -3573,7 +3583,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         launch_shadow(h, B, rec, n, counts, node0);
                         return;
                     }
-                    if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                    if (hipMemcpyAsync(h->host_mcount.data(), mc_sub, h->host_mcount.size() * sizeof(unsigned),
                                        hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                         stream_sync(h) != hipSuccess)
                         return;
@@ -3607,7 +3617,6 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                         int stl = 0;
                         while ((1 << stl) < h->subtile) ++stl;
                         const float* stb = h->stbox + 6 * (node0 >> stl);
-                        hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
                         hipError_t ue = hipSuccess;
                         {
                             KTimer tu(h, h->cur_st, 14);
@@ -3616,7 +3625,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                             for (uint64_t b0 = 0; b0 < tblocks && ue == hipSuccess; b0 += max_blocks) {
                                 uint32_t b0u = (uint32_t)b0;
                                 void* uargs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&stb, &h->slist, (void*)&s1seg,
-                                                 &b0u, (void*)&ssegcap, &h->light_sbox, &counts, &h->s2list, &h->mcount,
+                                                 &b0u, (void*)&ssegcap, &h->light_sbox, &counts, &h->s2list, &mc_subtile,
                                                  (void*)&s2segcap, &h->err, &h->jit_stats, &h->light_psamp2};
                                 ue = hipModuleLaunchKernel((hipFunction_t)h->jit_subtile, (unsigned)std::min(max_blocks, tblocks - b0),
                                                            1, 1, frt::kTraceBlock, 1, 1, 0, h->stream, uargs, nullptr);
@@ -3632,7 +3641,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                             launch_shadow(h, B, rec, n, counts, node0);
                             return;
                         }
-                        if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+                        if (hipMemcpyAsync(h->host_mcount.data(), mc_subtile, h->host_mcount.size() * sizeof(unsigned),
                                            hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                             stream_sync(h) != hipSuccess)
                             return;
@@ -3677,7 +3686,6 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 launch_shadow(h, B, rec, n, counts, node0);
                 return;
             }
-            hip_ignore(hipMemsetAsync(h->mcount, 0, kMixSegs * kMixLine * sizeof(unsigned), h->stream));
             hipError_t le = hipSuccess;
             {
                 KTimer tb(h, h->cur_st, 8);
@@ -3688,7 +3696,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     for (uint64_t b0 = 0; b0 < list_blocks && le == hipSuccess; b0 += max_blocks) {
                         uint32_t b0u = (uint32_t)b0;
                         void* largs[] = {&h->S, (void*)&B, (void*)&rec, &zero, &nn, (void*)&no_box, (void*)&list_in, &tseg, &b0u,
-                                         &list_segcap, (void*)&list_boxes, &counts, nout, &h->mcount, &segcap, &h->err,
+                                         &list_segcap, (void*)&list_boxes, &counts, nout, &mc_node, &segcap, &h->err,
                                          &h->jit_stats, &h->light_psamp2};
                         le = hipModuleLaunchKernel((hipFunction_t)h->jit_list, (unsigned)std::min(max_blocks, list_blocks - b0), 1, 1,
                                                    frt::kTraceBlock, 1, 1, 0, h->stream, largs, nullptr);
@@ -3701,7 +3709,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                     frt::jit::SegTable no_seg{};
                     uint32_t zero = 0;
                     void* bargs[] = {&h->S, (void*)&B, (void*)&rec, &np, &nn, (void*)&no_box, (void*)&no_list, &no_seg, &zero, &zero,
-                                     &h->light_aabb, &counts, nout, &h->mcount, &segcap, &h->err, &h->jit_stats,
+                                     &h->light_aabb, &counts, nout, &mc_node, &segcap, &h->err, &h->jit_stats,
                                      &h->light_psamp2};
                     le = hipModuleLaunchKernel((hipFunction_t)h->jit_beam, grid_for(npairs, frt::kTraceBlock), 1, 1,
                                                frt::kTraceBlock, 1, 1, 0, h->stream, bargs, nullptr);
@@ -3717,7 +3725,7 @@ static void launch_shadow(frt_scene_handle* h, const frt::Batch& B, const frt::S
                 launch_shadow(h, B, rec, n, counts, node0);
                 return;
             }
-            if (hipMemcpyAsync(h->host_mcount.data(), h->mcount, h->host_mcount.size() * sizeof(unsigned),
+            if (hipMemcpyAsync(h->host_mcount.data(), mc_node, h->host_mcount.size() * sizeof(unsigned),
                                hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                 stream_sync(h) != hipSuccess)
                 return;
@@ -4593,7 +4601,8 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             B.qprefix = d > 0 ? L.qprefix : nullptr;
             B.qsegcap = L.cap / kQueueSegs;
             B.next_segcap = N.cap / kQueueSegs;
-            FRT_HIP(hipMemsetAsync(L.counts, 0, (size_t)n * std::max(1, h->S.num_lights) * sizeof(int32_t), h->stream));
+            if (h->S.num_lights < 1)  // (k_prepare zeroes the level's counts of its nodes' lights)
+                FRT_HIP(hipMemsetAsync(L.counts, 0, (size_t)n * sizeof(int32_t), h->stream));
             if (grow(&h->hits, h->hits_cap, n)) return -1;
             if (!h->S.cfg.all_ni_one && grow(&h->hn12, h->hn12_cap, 2 * n)) return -1;
             double* hn12 = h->S.cfg.all_ni_one ? nullptr : h->hn12;
@@ -4618,7 +4627,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
                                    dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits, hn12,
                                    L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl,
-                                   subtiles ? h->stbox : nullptr, stl);
+                                   subtiles ? h->stbox : nullptr, stl, L.counts);
                 FRT_HIP(hipGetLastError());
             }
             // the next level's queue counts are final here (k_prepare appends the level's rays): their copy rides on
