@@ -724,6 +724,70 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                             }
                         }
                     };
+                    // Two light points at a time (FRT_SHADE_PAIR, default 1; the factored sums with the shared-term
+                    // vectors): each point's terms are one long dependent chain (two reciprocal square roots with their
+                    // Newton steps, the tail test's logarithms), and the per-point branches of the slow-path checks and
+                    // of the tail test kept the compiler from overlapping consecutive points. Here the two points'
+                    // chains run side by side up to the tail test, the slow paths and the specular terms sit behind one
+                    // ballot for both, and every lane computes the same values as term() and adds them to the sums in
+                    // the same order (point p before p + 1): bit-identical.
+#ifndef FRT_SHADE_PAIR
+#define FRT_SHADE_PAIR 1
+#endif
+                    constexpr bool kPair = FRT_SHADE_PAIR && kAlg && kFactored && FRT_SHADE_FAST;
+                    // the specular terms of one point past its tail test (term()'s arithmetic)
+                    auto spec_rest = [&](double ndl, double ndh, double edh, double ldh) {
+                        const double edh_inv = recip_shade(edh);
+                        const double dist_term = pow_apply(ndh, nsd, pplan) * cdist;
+                        const double gc = 2.0 * ndh * edh_inv;
+                        const double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
+                        const double om = 1.0 - ldh, om2 = om * om;
+                        const double factor = om2 * om2 * om;
+                        const double brdf = div_shade(dist_term * geo, 4.0 * ndl * ned);
+                        sum_b += brdf;
+                        sum_fb += factor * brdf;
+                    };
+                    auto term2 = [&](const double* lp0, const double* lp1) {
+                        double d0[3], d1[3];
+                        for (int k = 0; k < 3; ++k) {
+                            d0[k] = lp0[k] - nr.over_point[k];
+                            d1[k] = lp1[k] - nr.over_point[k];
+                        }
+                        const double m20 = dot3_shade(d0, d0), m21 = dot3_shade(d1, d1);
+                        double rl0 = rsqrt_nr(m20), rl1 = rsqrt_nr(m21);
+                        {
+                            const bool s0 = !shade_in_range(m20), s1 = !shade_in_range(m21);
+                            if (__builtin_expect(__ballot(s0 || s1) != 0ull, 0)) {
+                                if (s0) rl0 = 1.0 / sqrt(m20);
+                                if (s1) rl1 = 1.0 / sqrt(m21);
+                            }
+                        }
+                        const double ldn0 = dot3_shade(d0, nr.normalv) * rl0, ldn1 = dot3_shade(d1, nr.normalv) * rl1;
+                        if (S.cfg.include_diffuse && ldn0 >= 0.0) sum_ldn += ldn0;
+                        if (S.cfg.include_diffuse && ldn1 >= 0.0) sum_ldn += ldn1;
+                        if (!S.cfg.include_spec_highlight) return;
+                        const bool n0 = ldn0 >= 0.0, n1 = ldn1 >= 0.0;
+                        const double el0 = dot3_shade(d0, nr.eyev) * rl0, ll0 = (m20 * rl0) * rl0;
+                        const double el1 = dot3_shade(d1, nr.eyev) * rl1, ll1 = (m21 * rl1) * rl1;
+                        const double h20 = ll0 + 2.0 * el0 + ee, h21 = ll1 + 2.0 * el1 + ee;
+                        double rh0 = rsqrt_nr(h20), rh1 = rsqrt_nr(h21);
+                        {
+                            const bool s0 = n0 && !shade_in_range(h20), s1 = n1 && !shade_in_range(h21);
+                            if (__builtin_expect(__ballot(s0 || s1) != 0ull, 0)) {
+                                if (s0) rh0 = 1.0 / sqrt(h20);
+                                if (s1) rh1 = 1.0 / sqrt(h21);
+                            }
+                        }
+                        const double ndh0 = fmax(0.0, (ldn0 + ned) * rh0), ndh1 = fmax(0.0, (ldn1 + ned) * rh1);
+                        const bool t0 = ldn0 > 0x1p-100 &&
+                                        nsf * __log2f((float)ndh0) - 2.0f * __log2f((float)ldn0) + skip_c < 0.0f;
+                        const bool t1 = ldn1 > 0x1p-100 &&
+                                        nsf * __log2f((float)ndh1) - 2.0f * __log2f((float)ldn1) + skip_c < 0.0f;
+                        const bool g0 = n0 && !t0, g1 = n1 && !t1;
+                        if (__ballot(g0 || g1) == 0ull) return;
+                        if (g0) spec_rest(ldn0, ndh0, fmax(0.0, (el0 + ee) * rh0), (ll0 + el0) * rh0);
+                        if (g1) spec_rest(ldn1, ndh1, fmax(0.0, (el1 + ee) * rh1), (ll1 + el1) * rh1);
+                    };
                     const double* row0 = S.light_points + L.points;
                     const int ns = L.num_samples;
                     // a wave-uniform row: the same point in every lane, so its address is wave-uniform and the loads go
@@ -745,7 +809,23 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                                                                (int)(uint32_t)((uint64_t)up >> 32))
                                                            << 32));
                         double a[3] = {sp[0], sp[1], sp[2]};
-                        for (int p = 0; p < ns; ++p) {  // (the next point's scalar loads ahead of this one's arithmetic)
+                        int p = 0;
+                        if (kPair) {  // (pairs of points, the next pair's scalar loads ahead of this pair's arithmetic)
+                            const const_pts q1 = sp + 3 * min(1, ns - 1);
+                            double b[3] = {q1[0], q1[1], q1[2]};
+                            for (; p + 1 < ns; p += 2) {
+                                const double lp0[3] = {a[0], a[1], a[2]}, lp1[3] = {b[0], b[1], b[2]};
+                                const const_pts qa = sp + 3 * min(p + 2, ns - 1), qb = sp + 3 * min(p + 3, ns - 1);
+                                a[0] = qa[0];
+                                a[1] = qa[1];
+                                a[2] = qa[2];
+                                b[0] = qb[0];
+                                b[1] = qb[1];
+                                b[2] = qb[2];
+                                term2(lp0, lp1);
+                            }
+                        }
+                        for (; p < ns; ++p) {  // (the next point's scalar loads ahead of this one's arithmetic)
                             const double lp[3] = {a[0], a[1], a[2]};
                             const const_pts q = sp + 3 * min(p + 1, ns - 1);
                             a[0] = q[0];
