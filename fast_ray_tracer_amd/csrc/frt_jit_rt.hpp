@@ -338,6 +338,33 @@ __device__ __forceinline__ void count_part(const DevScene& S, const Lane32& L, b
     }
 }
 
+// The beam stages' decided lit pairs add their sample count to every node of their tile (sub-tile): lanes of one wave
+// that share the tile — the sub-part stage's 16 samples of a tile pair, the tile stage's parts of one tile — first sum
+// their counts, then the wave adds each (run, light) group's total with one atomic per node, the run's nodes spread
+// over the lanes (one per lane for 64-node tiles), instead of one atomic per node and lit lane (up to 64 per lane on
+// the same addresses). Integer sums: the counts are the same. (all lanes of the wave; base, len, lt: the run's first
+// node, its length (uniform) and light)
+__device__ __forceinline__ void add_run_counts(const ShadowHead* __restrict__ shead, int32_t* counts, uint32_t nl,
+                                               bool add, uint32_t base, uint32_t len, uint32_t lt, int32_t amount,
+                                               uint32_t nnodes) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long pending = __ballot(add);
+    while (pending) {
+        const int ld = __builtin_ctzll(pending);
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)base, ld);
+        const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)lt, ld);
+        const bool same = add && base == b0 && lt == l0;
+        pending &= ~__ballot(same);
+        int32_t v = same ? amount : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        for (uint32_t n = (uint32_t)lane; n < len; n += 64u) {
+            const uint32_t nd = b0 + n;
+            if (nd < nnodes && shead[nd].material >= 0) atomicAdd(counts + nd * nl + l0, v);
+        }
+    }
+}
+
 // the lit lanes of each run of consecutive valid lanes with the same (node, light) (the per-ray kernel's node-major
 // lanes: a node's samples of several list entries side by side), one atomic per run by its first lane (all lanes of
 // the wave)
