@@ -724,7 +724,8 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                             }
                         }
                     };
-                    // Two light points at a time (FRT_SHADE_PAIR, default 1; the factored sums with the shared-term
+                    // Two light points at a time (FRT_SHADE_PAIR=1 builds, off by default: k_shade_lit 8.85 -> 9.0 ms
+                    // per headline frame with it, profiles/r06_ab_shade_pair.txt; the factored sums with the shared-term
                     // vectors): each point's terms are one long dependent chain (two reciprocal square roots with their
                     // Newton steps, the tail test's logarithms), and the per-point branches of the slow-path checks and
                     // of the tail test kept the compiler from overlapping consecutive points. Here the two points'
@@ -732,7 +733,7 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     // ballot for both, and every lane computes the same values as term() and adds them to the sums in
                     // the same order (point p before p + 1): bit-identical.
 #ifndef FRT_SHADE_PAIR
-#define FRT_SHADE_PAIR 1
+#define FRT_SHADE_PAIR 0
 #endif
                     constexpr bool kPair = FRT_SHADE_PAIR && kAlg && kFactored && FRT_SHADE_FAST;
                     // the specular terms of one point past its tail test (term()'s arithmetic)
