@@ -558,14 +558,21 @@ def main():
                  "render_multi(sc, devices=%r); print('RM', 1e3 * (time.perf_counter() - t0), "
                  "jit_cache_stats()['compiles']); print('PH', json.dumps(render_multi_phases()))"
                  % (ROOT, os.path.join(GOLDEN, "scenes", args.scene + ".c"), ASSETS, str(local_rank)))
-        pr = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, timeout=300)
-        lines = [ln.split() for ln in pr.stdout.splitlines() if ln.startswith("RM ")]
-        if pr.returncode == 0 and lines:
-            rm["render_multi_wall_ms_second_process"] = round(float(lines[-1][1]), 2)
-            rm["render_multi_second_process_compiles"] = int(lines[-1][2])
+        # three such processes, one after the other: the median (a fresh process's HIP initialisation varies by box)
+        probes = []
+        for _ in range(3):
+            pr = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, timeout=300)
+            lines = [ln.split() for ln in pr.stdout.splitlines() if ln.startswith("RM ")]
             ph = [ln[3:] for ln in pr.stdout.splitlines() if ln.startswith("PH ")]
-            if ph:
-                rm["render_multi_phases_second_process"] = json.loads(ph[-1])
+            if pr.returncode == 0 and lines and ph:
+                probes.append((float(lines[-1][1]), int(lines[-1][2]), json.loads(ph[-1])))
+        if probes:
+            probes.sort(key=lambda x: x[0])
+            med = probes[len(probes) // 2]
+            rm["render_multi_wall_ms_second_process"] = round(med[0], 2)
+            rm["render_multi_wall_ms_second_process_runs"] = [round(x[0], 2) for x in probes]
+            rm["render_multi_second_process_compiles"] = max(x[1] for x in probes)
+            rm["render_multi_phases_second_process"] = med[2]  # (the median process's phases)
         ndev = torch.cuda.device_count()
         if ndev > 1:  # the in-process multi-GPU path of render_multi (one host thread per device)
             t0 = time.perf_counter()
