@@ -3462,6 +3462,16 @@ static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::Qu
                     hip_ignore(hipStreamSynchronize(h->stream));
                     std::fprintf(stderr, "frt: frt_jit_trace level %d: %lld rays, %u to the generic walk\n", B.level,
                                  (long long)n, c);
+                    // (FRT_JIT_TRACE_DUMP=<path>: the level-0 list of undecided rays, int32 ray indices, for analysis)
+                    const char* dump = std::getenv("FRT_JIT_TRACE_DUMP");
+                    if (dump && B.level == 0 && c > 0) {
+                        std::vector<int32_t> v(std::min<size_t>(c, cap));
+                        hip_ignore(hipMemcpy(v.data(), h->tredo, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+                        if (FILE* f = std::fopen(dump, "wb")) {
+                            std::fwrite(v.data(), sizeof(int32_t), v.size(), f);
+                            std::fclose(f);
+                        }
+                    }
                 }
                 return;
             }
