@@ -19,12 +19,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import device_source_sha  # noqa: E402  (bench.py's pairing rule: latest_pmc)
 
 out, kre, workload = sys.argv[1], sys.argv[2], sys.argv[3]
+# the kernel's own name, not a longer one it prefixes ("frt_jit_sub" is not "frt_jit_subtile", "k_shade" not
+# "k_shade_lit"): the name bounded by characters that cannot continue an identifier
+kpat = re.compile(r"(?<![A-Za-z0-9_])(?:%s)(?![A-Za-z0-9_])" % kre)
 # the device sources this pass measured (bench.py pairs a summary only with live times of the same sources)
 res = {"kernel": sys.argv[4] if len(sys.argv) > 4 else kre, "workload": workload,
        "device_source_sha16": device_source_sha()}
 for f in glob.glob(out + "/kt/**/*kernel_stats.csv", recursive=True):
     for row in csv.DictReader(open(f)):
-        if re.search(kre, row["Name"]):
+        if kpat.search(row["Name"]):
             res["rocprof_avg_ms"] = float(row["AverageNs"]) / 1e6
             res["rocprof_calls"] = int(row["Calls"])
             res["rocprof_percentage"] = float(row["Percentage"])
@@ -35,7 +38,7 @@ for d in sorted(os.listdir(out)):
     disp = collections.defaultdict(set)
     for f in glob.glob("%s/%s/**/*counter_collection.csv" % (out, d), recursive=True):
         for row in csv.DictReader(open(f)):
-            if re.search(kre, row["Kernel_Name"]):
+            if kpat.search(row["Kernel_Name"]):
                 tot[row["Counter_Name"]] += float(row["Counter_Value"])
                 disp[row["Counter_Name"]].add(row["Dispatch_Id"])
     for k, v in tot.items():
