@@ -11,7 +11,7 @@ from conftest import load_scene  # noqa: E402
 sc = load_scene(sys.argv[1])
 x, y = int(sys.argv[2]), int(sys.argv[3])
 sub = int(sys.argv[4]) if len(sys.argv) > 4 else 0
-os.environ["FRT_JIT_TRACE_DBG"] = str((y * sc.width + x) * sc.spp + sub)
+os.environ["FRT_JIT_TRACE_DBG"] = str(x * sc.spp + sub)  # (the kernel's index within the batch: row y alone)
 os.environ["FRT_JIT_CACHE"] = "0"
 from fast_ray_tracer_amd.runtime import GpuRenderer  # noqa: E402
 
