@@ -1197,8 +1197,11 @@ __device__ __forceinline__ void combine_node(const DevScene& S, const int32_t* _
         // reflected / refracted_color from the children's slots; a child that was not traced
         // (zero weight, or nothing to spawn) contributes an exact 0
         double R[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, T[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (nr.flags & kReflSpawned) tri_load(child, 2 * i, R);
-        if (nr.flags & kRefrSpawned) tri_load(child, 2 * i + 1, T);
+        // (a level's child slots as two halves of its child columns, reflected then refracted: slot s of node i at
+        // s * cap / 2 + i, so the child level's stores and this level's loads run along consecutive nodes)
+        const int64_t half = child.cap >> 1;
+        if (nr.flags & kReflSpawned) tri_load(child, i, R);
+        if (nr.flags & kRefrSpawned) tri_load(child, half + i, T);
         double rl[12], rr[12];
         for (int t = 0; t < 12; t += 4) {
             for (int k = 0; k < 3; ++k) {
@@ -1240,7 +1243,8 @@ __global__ void __launch_bounds__(kBlock) k_combine(DevScene S, const int32_t* _
     double col[12];
     combine_node(S, counts, nr, i, surface, child, mats, include_specular, col, spos);
     if (nr.parent >= 0) {
-        tri_store(parent_child, 2 * (int64_t)nr.parent + nr.slot, col);  // a missed child writes its zeros
+        // (a missed child writes its zeros; slot halves as combine_node reads them)
+        tri_store(parent_child, (int64_t)nr.slot * (parent_child.cap >> 1) + nr.parent, col);
     } else {
         tri_store(sample_out, i, col);  // sample order (pixel-major): one coalesced run per column
     }
@@ -2065,7 +2069,7 @@ struct frt_scene_handle {
         frt::ShadowHead* head = nullptr;
         frt::QueuedRay* q = nullptr;
         frt::Cols<frt::Tri9> surface;
-        frt::Cols<frt::Tri9> child;  // two slots per node: 2 i (reflected), 2 i + 1 (refracted)
+        frt::Cols<frt::Tri9> child;  // two slots per node: i (reflected), cap + i (refracted), cap = the level's
         int64_t* qprefix = nullptr;                     // queue segments of this level (frt_shadow.hpp)
         std::vector<int64_t> hprefix = std::vector<int64_t>(frt::kQueueSegs + 1, 0);
         int32_t* counts = nullptr;
