@@ -978,6 +978,19 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
     }
 }
 
+// A secondary level's queue entries with their parent-order keys (the reflected children first, then the
+// refracted, each in parent order) and storage slots, for the radix sort behind Batch.qperm (FRT_QUEUE_SORT).
+// B: the level's queue segments (qprefix, qsegcap).
+__global__ void __launch_bounds__(kBlock) k_queue_keys(Batch B, const QueuedRay* __restrict__ q, int64_t n, int pbits,
+                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ slots) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t s = queue_slot(B, i);
+    const QueuedRay& qr = q[s];
+    keys[i] = ((uint32_t)(qr.slot & 1) << pbits) | (uint32_t)qr.parent;
+    slots[i] = (uint32_t)s;
+}
+
 // With a multi-row light (the shipped area-light cache: 65 535 rows of 100 points, 157 MB) every listed node reads
 // the row its shading draw picks, 2.4 KB of the cache per node and a different row in every lane (22 GB fetched per
 // headline-size launch, memory-bound). The list is put in row order first (k_lit_rows lists the nodes densely with
@@ -2057,6 +2070,9 @@ struct frt_scene_handle {
     int64_t lit_flat_cap = 0;
     frt::LitStage* lit_stage = nullptr;  // (k_lit_stage's records, FRT_SHADE_STAGE)
     int64_t lit_stage_cap = 0;
+    int queue_sort = 1;                 // a level's queue read in parent order (FRT_QUEUE_SORT=0: the segments' order)
+    uint32_t* qsort = nullptr;          // (its keys, their alternate buffer and the storage slots, 3 words per entry)
+    int64_t qsort_cap = 0;
     unsigned char* scan_tmp = nullptr;  // (the device sort's temporary storage)
     int64_t scan_tmp_cap = 0;
     unsigned* shade_lcount = nullptr;
@@ -2075,6 +2091,9 @@ struct frt_scene_handle {
         int32_t* counts = nullptr;
         uint32_t* spos = nullptr;  // (lit nodes shaded from staged records: a node's sorted position, k_shade_lit)
         bool staged = false;       // this batch's shading of the level went through k_lit_stage
+        uint32_t* qperm = nullptr;  // (the queue in parent order, k_queue_keys + radix sort; qperm_cap entries)
+        int64_t qperm_cap = 0;
+        bool sorted = false;        // this batch's queue of the level is read through qperm
         int64_t cap = 0;
     };
     std::vector<Level> levels;
@@ -2784,6 +2803,19 @@ size_t frt_frame_stats_size(void) { return sizeof(frt_frame_stats); }
 static std::mutex g_warm_mu;
 static hipStream_t g_warm_stream[64] = {};
 
+void* frt_host_pinned_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void frt_host_pinned_free(void* p) {
+    if (p) hip_ignore(hipHostFree(p));
+}
+
 int frt_device_warmup(int device) {
     // (FRT_WARMUP_TRACE: each step's time to stderr)
     static const bool trace = std::getenv("FRT_WARMUP_TRACE") != nullptr;
@@ -3140,6 +3172,11 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         // round 5 did. Shipped frame: shade 14.2 / 13.1 / 12.9 ms for 0 / 1 / 2 (profiles/r06_ab_shipped_modes.txt)
         const char* se = std::getenv("FRT_SHADE_STAGE");
         h->shade_stage = h->sort_light >= 0 ? (se ? std::atoi(se) : 2) : 0;
+        // the secondary levels' queues read in parent order (reflected children, then refracted): a k_prepare
+        // block appends to segment blockIdx % kQueueSegs, so the segments' order puts children of pixels 256 apart
+        // side by side, and the shadow pass's tiles of consecutive nodes spread over the scene
+        const char* qs = std::getenv("FRT_QUEUE_SORT");
+        h->queue_sort = qs ? std::atoi(qs) : 1;
     }
     // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
     // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L
@@ -3262,6 +3299,7 @@ void frt_scene_release(frt_scene_handle* h) {
         hip_ignore(hipFree(L.counts));
         hip_ignore(hipFree(L.spos));
         hip_ignore(hipFree(L.qprefix));
+        hip_ignore(hipFree(L.qperm));
     }
     hip_ignore(hipFree(h->hits));
     hip_ignore(hipFree(h->hn12));
@@ -3291,6 +3329,7 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->shade_lcount));
     hip_ignore(hipFree(h->lit_row));
     hip_ignore(hipFree(h->lit_flat));
+    hip_ignore(hipFree(h->qsort));
     hip_ignore(hipFree(h->lit_stage));
     hip_ignore(hipFree(h->scan_tmp));
     hip_ignore(hipFree(h->mixed));
@@ -4486,6 +4525,7 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
                                G.gq);
             frt::Batch Bg = B;  // the gather rays form one contiguous queue
             Bg.qprefix = nullptr;
+            Bg.qperm = nullptr;
             launch_trace(h, Bg, G.gq, rays, G.ghits, 0);
             // FRT_GATHER_QUEUE=0: the static request ranges (A/B runs)
             const char* qenv = std::getenv("FRT_GATHER_QUEUE");
@@ -4694,6 +4734,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             if (ensure_level(h, d + 1, 2 * n + (int64_t)kQueueSegs * 2 * kBlock)) return -1;
             auto& N = h->levels[d + 1];
             B.qprefix = d > 0 ? L.qprefix : nullptr;
+            B.qperm = d > 0 && L.sorted ? L.qperm : nullptr;
             B.qsegcap = L.cap / kQueueSegs;
             B.next_segcap = N.cap / kQueueSegs;
             if (h->S.num_lights < 1)  // (k_prepare zeroes the level's counts of its nodes' lights)
@@ -4856,6 +4897,30 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 FRT_HIP(hipMemcpyAsync(N.qprefix, N.hprefix.data(), (kQueueSegs + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
                                        h->stream));
             count[d + 1] = d < path ? next : 0;
+            // the next level in parent order (FRT_QUEUE_SORT): its nodes, tiles and shading then follow the
+            // parents' pixels; keys: refracted bit above the parent index
+            int pbits = 1;
+            while (pbits < 32 && (1ll << pbits) < n) ++pbits;
+            N.sorted = h->queue_sort != 0 && d < path && next >= 4096 && !overflow && pbits < 32 &&
+                       N.cap <= (int64_t)UINT32_MAX;
+            if (N.sorted) {
+                KTimer t(h, st, 6);
+                if (grow(&h->qsort, h->qsort_cap, 3 * next) || grow(&N.qperm, N.qperm_cap, next)) return -1;
+                uint32_t *keys = h->qsort, *keys2 = h->qsort + next, *slots = h->qsort + 2 * next;
+                Batch Bn = B;
+                Bn.qprefix = N.qprefix;
+                Bn.qsegcap = N.cap / kQueueSegs;
+                Bn.qperm = nullptr;
+                hipLaunchKernelGGL(k_queue_keys, dim3(grid_for(next)), dim3(kBlock), 0, h->stream, Bn, N.q, next, pbits,
+                                   keys, slots);
+                FRT_HIP(hipGetLastError());
+                size_t tmp_bytes = 0;
+                FRT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, slots, N.qperm, (int)next, 0,
+                                                           pbits + 1, h->stream));
+                if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
+                FRT_HIP(hipcub::DeviceRadixSort::SortPairs((void*)h->scan_tmp, tmp_bytes, keys, keys2, slots, N.qperm,
+                                                           (int)next, 0, pbits + 1, h->stream));
+            }
             if (st) {
                 if (d > 0) st->secondary_rays += (uint64_t)n;
                 else st->primary_rays += (uint64_t)n;

@@ -50,10 +50,12 @@ struct Batch {
     const int64_t* qprefix;  // this level's queue segments (kQueueSegs + 1 prefix counts); null: contiguous
     int64_t qsegcap;         // entries per segment of this level's queue
     int64_t next_segcap;     // entries per segment of the next level's queue
+    const uint32_t* qperm;   // the level's entries in parent order: entry i at storage slot qperm[i]; null: the segments
 };
 
 // storage slot of entry i of the level's queue
 __device__ __forceinline__ int64_t queue_slot(const Batch& B, int64_t i) {
+    if (B.qperm != nullptr) return B.qperm[i];
     if (B.qprefix == nullptr) return i;
     int lo = 0, hi = kQueueSegs;  // the last segment j with qprefix[j] <= i
     while (hi - lo > 1) {
