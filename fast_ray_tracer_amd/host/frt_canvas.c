@@ -9,6 +9,7 @@
  * the device canvas has been copied back.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -19,19 +20,91 @@
 #include "src/libs/canvas/canvas.h"
 #include "src/color/rgb.h"
 #include "src/libs/linalg/linalg.h"
+#include "frt_device.h"
 
 #define FRT_SQRT3 1.7320508075688772
+
+/*
+ * A canvas with a word of our own behind the reference's struct: the byte size of its array when that array is
+ * page-locked (frt_canvas_alloc_pinned), 0 when malloc'd. render_multi's canvas is page-locked so that the device's
+ * copy of the frame is one DMA into it (into malloc'd memory the runtime stages it through its own buffers, and a
+ * fresh 66 MB array at 1920x1080 first takes ~16 000 page faults); canvas_free hands such an array to a one-entry
+ * pool that the next render_multi of the same size takes again.
+ */
+typedef struct {
+    struct canvas c;
+    size_t pinned_bytes;
+} canvas_box;
+
+static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
+static void *g_pool_arr;     /* an idle page-locked array */
+static size_t g_pool_bytes;
+
+static Canvas
+canvas_new(size_t width, size_t height, bool super_sample, void (*color_space_fn)(const Color, Color))
+{
+    canvas_box *b = (canvas_box *)malloc(sizeof(canvas_box));
+    if (b == NULL) {
+        return NULL;
+    }
+    b->pinned_bytes = 0;
+    b->c.arr = NULL;
+    b->c.width = width;
+    b->c.height = height;
+    b->c.super_sample = super_sample;
+    b->c.color_space_fn = color_space_fn;
+    return &b->c;
+}
 
 Canvas
 canvas_alloc(size_t width, size_t height, bool super_sample, void (*color_space_fn)(const Color, Color))
 {
-    Canvas c = (Canvas)malloc(sizeof(struct canvas));
-    c->arr = (Color *)malloc(width * height * sizeof(Color));
-    c->width = width;
-    c->height = height;
-    c->super_sample = super_sample;
-    c->color_space_fn = color_space_fn;
+    Canvas c = canvas_new(width, height, super_sample, color_space_fn);
+    if (c != NULL) {
+        c->arr = (Color *)malloc(width * height * sizeof(Color));
+    }
     return c;
+}
+
+Canvas
+frt_canvas_alloc_pinned(size_t width, size_t height, bool super_sample, void (*color_space_fn)(const Color, Color))
+{
+    Canvas c = canvas_new(width, height, super_sample, color_space_fn);
+    if (c == NULL) {
+        return NULL;
+    }
+    const size_t bytes = width * height * sizeof(Color);
+    void *stale = NULL;
+    pthread_mutex_lock(&g_pool_lock);
+    if (g_pool_arr != NULL && g_pool_bytes == bytes) {
+        c->arr = (Color *)g_pool_arr;
+        g_pool_arr = NULL;
+    } else {
+        stale = g_pool_arr;  /* (another size: freed, outside the lock) */
+        g_pool_arr = NULL;
+    }
+    pthread_mutex_unlock(&g_pool_lock);
+    frt_host_pinned_free(stale);
+    if (c->arr == NULL) {
+        c->arr = (Color *)frt_host_pinned_alloc(bytes);
+    }
+    if (c->arr != NULL) {
+        ((canvas_box *)c)->pinned_bytes = bytes;
+    } else {
+        c->arr = (Color *)malloc(bytes);  /* (no page-locked memory: an ordinary array) */
+    }
+    return c;
+}
+
+void
+frt_canvas_pool_release(void)
+{
+    pthread_mutex_lock(&g_pool_lock);
+    void *p = g_pool_arr;
+    g_pool_arr = NULL;
+    g_pool_bytes = 0;
+    pthread_mutex_unlock(&g_pool_lock);
+    frt_host_pinned_free(p);
 }
 
 Ppm
@@ -46,10 +119,24 @@ ppm_alloc(size_t len)
 void
 canvas_free(Canvas c)
 {
-    if (c) {
-        free(c->arr);
-        free(c);
+    if (c == NULL) {
+        return;
     }
+    canvas_box *b = (canvas_box *)c;
+    if (b->pinned_bytes > 0) {
+        void *spill = c->arr;
+        pthread_mutex_lock(&g_pool_lock);
+        if (g_pool_arr == NULL) {
+            g_pool_arr = c->arr;
+            g_pool_bytes = b->pinned_bytes;
+            spill = NULL;
+        }
+        pthread_mutex_unlock(&g_pool_lock);
+        frt_host_pinned_free(spill);
+    } else {
+        free(c->arr);
+    }
+    free(b);
 }
 
 void

@@ -372,6 +372,7 @@ frt_render_multi_release(void)
     pthread_mutex_lock(&g_rm_lock);
     release_kept();
     pthread_mutex_unlock(&g_rm_lock);
+    frt_canvas_pool_release();
 }
 
 /* the phases of the last render_multi on this process, in ms (frt_render_multi_phases) */
@@ -426,13 +427,14 @@ render_multi_locked(Camera cam, World w, size_t usteps, size_t vsteps, bool jitt
     const double rm0 = now_ms();
     memset(g_rm_phases, 0, sizeof(g_rm_phases));
     const size_t width = cam != NULL ? cam->hsize : 1, height = cam != NULL ? cam->vsize : 1;
-    /* (the canvas is zeroed only where a failure leaves it unwritten: a successful render writes every pixel) */
-    Canvas c = canvas_alloc(width, height, false, NULL);
     int dev[FRT_MAX_RENDER_DEVICES];
     char err[512];
     frt_scene fs;
     g_render_error[0] = '\0';
     const int n = render_devices(dev, FRT_MAX_RENDER_DEVICES, err, sizeof(err));
+    /* (the canvas is zeroed only where a failure leaves it unwritten: a successful render writes every pixel; with
+     * devices its array is page-locked, so one device's frame lands in it by DMA) */
+    Canvas c = n > 0 ? frt_canvas_alloc_pinned(width, height, false, NULL) : canvas_alloc(width, height, false, NULL);
     if (n < 0) {
         fprintf(stderr, "frt: render_multi cannot run on the GPU: %s\n", err);
         snprintf(g_render_error, sizeof(g_render_error), "%s", err);

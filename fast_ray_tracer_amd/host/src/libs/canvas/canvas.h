@@ -29,6 +29,12 @@ Ppm ppm_alloc(size_t len);
 void canvas_free(Canvas c);
 void ppm_free(Ppm p);
 
+/* (frt: render_multi's canvas, its array in page-locked memory that the device writes by DMA; canvas_free hands the
+ * array to a one-entry pool the next such canvas of the same size reuses. frt_canvas_pool_release frees the pooled
+ * array: frt_render_multi_release calls it) */
+Canvas frt_canvas_alloc_pinned(size_t width, size_t height, bool super_sample, void (*color_space_fn)(const Color, Color));
+void frt_canvas_pool_release(void);
+
 void canvas_write_pixels(Canvas c, int col, int row, Color *colors, size_t num);
 void canvas_write_pixel(Canvas c, int col, int row, Color color);
 void canvas_pixel_at(Canvas c, int col, int row, Color res);

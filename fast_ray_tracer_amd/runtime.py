@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 import threading
 
 import numpy as np
@@ -234,14 +235,18 @@ def render_multi(scene: Scene, devices: str | None = None) -> np.ndarray:
                 os.environ.pop("FRT_DEVICES", None)
             else:
                 os.environ["FRT_DEVICES"] = old
+    # the canvas's array itself, not a copy (a 1920x1080 canvas is 66 MB): the returned array owns the canvas, and
+    # canvas_free runs when it is collected (render_multi's array goes back to host/frt_canvas.c's pinned pool)
     try:
-        # struct canvas (canvas.h): size_t width, height; bool super_sample; ...; Color *arr — read via the helper
+        # struct canvas (canvas.h): Color *arr; size_t width, height; ... — read via the helper
         lib.frt_canvas_data.restype = ctypes.POINTER(ctypes.c_double)
         lib.frt_canvas_data.argtypes = [vp]
         ptr = lib.frt_canvas_data(c)
-        out = np.ctypeslib.as_array(ptr, shape=(scene.height, scene.width, 4)).copy()
-    finally:
+        out = np.ctypeslib.as_array(ptr, shape=(scene.height, scene.width, 4))
+        weakref.finalize(out, lib.canvas_free, c)
+    except BaseException:
         lib.canvas_free(c)
+        raise
     lib.frt_render_multi_error.restype = ctypes.c_char_p
     err = lib.frt_render_multi_error()
     global _release_registered

@@ -245,6 +245,13 @@ int frt_device_count(void);
  * while it flattens the scene); returns 0, or -1 when the device cannot be set */
 int frt_device_warmup(int device);
 
+/* page-locked host memory (hipHostMalloc) for render_multi's canvas array, which the device then writes by DMA
+ * instead of through the runtime's staging copies into pageable memory (the reference's canvas_alloc mallocs it,
+ * src/libs/canvas/canvas.c:21-24; canvas_free hands it back, canvas.c:54); NULL when it cannot be allocated.
+ * frt_host_pinned_free releases it (NULL: nothing) */
+void *frt_host_pinned_alloc(size_t bytes);
+void frt_host_pinned_free(void *p);
+
 /* sizeof(frt_frame_stats) as this library was built: a caller's mirror of the struct (runtime.py FrameStats)
  * checks its size against it before passing one in (no device needed) */
 size_t frt_frame_stats_size(void);

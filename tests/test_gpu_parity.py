@@ -500,3 +500,41 @@ def test_render_multi_concurrent_calls(built):
     assert not errs, errs
     for k in (0, 1):
         assert len(got[k]) == 3 and all(np.array_equal(g, ref[k]) for g in got[k])
+
+
+def test_render_multi_canvas_is_pinned_and_pooled(built):
+    """render_multi's canvas array is page-locked and pooled (host/frt_canvas.c frt_canvas_alloc_pinned): a freed
+    canvas's array is taken again by the next canvas of the same size, never while a canvas still holds it; the array
+    runtime.render_multi returns is the canvas itself (no copy) and its canvas is freed when it is collected."""
+    import ctypes
+    import gc
+    from fast_ray_tracer_amd.runtime import host_lib, release_render_multi, render_multi
+    lib = host_lib()
+    vp = ctypes.c_void_p
+    lib.frt_canvas_alloc_pinned.restype = vp
+    lib.frt_canvas_alloc_pinned.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_bool, vp]
+    lib.canvas_free.argtypes = [vp]
+    lib.frt_canvas_data.restype = vp
+    lib.frt_canvas_data.argtypes = [vp]
+    release_render_multi()  # (an empty pool)
+    c1 = lib.frt_canvas_alloc_pinned(64, 32, False, None)
+    c2 = lib.frt_canvas_alloc_pinned(64, 32, False, None)
+    a1, a2 = lib.frt_canvas_data(c1), lib.frt_canvas_data(c2)
+    assert a1 and a2 and a1 != a2
+    lib.canvas_free(c1)
+    c3 = lib.frt_canvas_alloc_pinned(64, 32, False, None)
+    assert lib.frt_canvas_data(c3) == a1  # (c1's array, from the pool)
+    c4 = lib.frt_canvas_alloc_pinned(16, 16, False, None)  # (another size, the pool empty: a fresh array)
+    assert lib.frt_canvas_data(c4) not in (a1, a2)
+    for c in (c2, c3, c4):
+        lib.canvas_free(c)
+    sc = load_scene("cornell_direct_64_4x4")
+    x = render_multi(sc, devices="0")
+    y = render_multi(sc, devices="0")
+    px = x.ctypes.data
+    assert y.ctypes.data != px and np.array_equal(x, y)
+    del x
+    gc.collect()
+    z = render_multi(sc, devices="0")
+    assert z.ctypes.data == px and np.array_equal(z, y)
+    release_render_multi()
