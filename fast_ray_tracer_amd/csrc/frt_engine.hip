@@ -981,13 +981,15 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
 // A secondary level's queue entries with their parent-order keys (the reflected children first, then the
 // refracted, each in parent order) and storage slots, for the radix sort behind Batch.qperm (FRT_QUEUE_SORT).
 // B: the level's queue segments (qprefix, qsegcap).
+// (shift: the parents' low bits left out of the key, runs of 2^shift parents in the segments' order)
 __global__ void __launch_bounds__(kBlock) k_queue_keys(Batch B, const QueuedRay* __restrict__ q, int64_t n, int pbits,
-                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ slots) {
+                                                       int shift, uint32_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ slots) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t s = queue_slot(B, i);
     const QueuedRay& qr = q[s];
-    keys[i] = ((uint32_t)(qr.slot & 1) << pbits) | (uint32_t)qr.parent;
+    keys[i] = ((uint32_t)(qr.slot & 1) << (pbits - shift)) | ((uint32_t)qr.parent >> shift);
     slots[i] = (uint32_t)s;
 }
 
@@ -2071,6 +2073,7 @@ struct frt_scene_handle {
     frt::LitStage* lit_stage = nullptr;  // (k_lit_stage's records, FRT_SHADE_STAGE)
     int64_t lit_stage_cap = 0;
     int queue_sort = 1;                 // a level's queue read in parent order (FRT_QUEUE_SORT=0: the segments' order)
+    int queue_sort_shift = 0;           // (FRT_QUEUE_SORT_SHIFT)
     uint32_t* qsort = nullptr;          // (its keys, their alternate buffer and the storage slots, 3 words per entry)
     int64_t qsort_cap = 0;
     unsigned char* scan_tmp = nullptr;  // (the device sort's temporary storage)
@@ -3177,6 +3180,8 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         // side by side, and the shadow pass's tiles of consecutive nodes spread over the scene
         const char* qs = std::getenv("FRT_QUEUE_SORT");
         h->queue_sort = qs ? std::atoi(qs) : 1;
+        const char* qsh = std::getenv("FRT_QUEUE_SORT_SHIFT");  // (A/B runs: parents' low bits out of the key)
+        h->queue_sort_shift = qsh ? std::max(0, std::min(16, std::atoi(qsh))) : 0;
     }
     // path-node keys carry a 12-bit heap code (k_prepare: children 2c, 2c + 1 of code c, root 1) and
     // the per-segment counter lines hold the level queue counts in words 0..15: a path of length L
@@ -4911,15 +4916,16 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 Bn.qprefix = N.qprefix;
                 Bn.qsegcap = N.cap / kQueueSegs;
                 Bn.qperm = nullptr;
+                const int shift = std::min(h->queue_sort_shift, pbits - 1);
                 hipLaunchKernelGGL(k_queue_keys, dim3(grid_for(next)), dim3(kBlock), 0, h->stream, Bn, N.q, next, pbits,
-                                   keys, slots);
+                                   shift, keys, slots);
                 FRT_HIP(hipGetLastError());
                 size_t tmp_bytes = 0;
                 FRT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, slots, N.qperm, (int)next, 0,
-                                                           pbits + 1, h->stream));
+                                                           pbits - shift + 1, h->stream));
                 if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
                 FRT_HIP(hipcub::DeviceRadixSort::SortPairs((void*)h->scan_tmp, tmp_bytes, keys, keys2, slots, N.qperm,
-                                                           (int)next, 0, pbits + 1, h->stream));
+                                                           (int)next, 0, pbits - shift + 1, h->stream));
             }
             if (st) {
                 if (d > 0) st->secondary_rays += (uint64_t)n;
