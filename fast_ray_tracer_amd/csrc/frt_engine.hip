@@ -305,7 +305,8 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
                                              int64_t n, const HitRec* __restrict__ hits, const double* __restrict__ hn12,
                                              NodeCols& rec,
                                              ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q,
-                                             unsigned long long* counters, unsigned* err, int64_t node, double* op) {
+                                             unsigned long long* counters, unsigned* err, int64_t node, double* op,
+                                             int* spawned = nullptr) {
     // this block's counter line: next-level queue segment count (word level + 1), pruned (16), hits (17)
     unsigned long long* line = counters + kCounterLine * (blockIdx.x % kQueueSegs);
     const int64_t seg_base = (int64_t)(blockIdx.x % kQueueSegs) * B.next_segcap;
@@ -405,15 +406,18 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
         const bool want_refr = refract_applies && !tf_zero;
         if (want_refl) flags |= kReflSpawned;
         if (want_refr) flags |= kRefrSpawned;
-        // slots in this block's segment of the next level's queue
-        const unsigned long long at_refl = wave_append(line + B.level + 1, want_refl);
-        const unsigned long long at_refr = wave_append(line + B.level + 1, want_refr);
+        // slots in this block's segment of the next level's queue; dense (spawned != nullptr): the fixed slots
+        // node (reflected) and n + node (refracted), no atomics, the caller records which are taken
+        const bool dense = spawned != nullptr;
+        const unsigned long long at_refl = dense ? 0ull : wave_append(line + B.level + 1, want_refl);
+        const unsigned long long at_refr = dense ? 0ull : wave_append(line + B.level + 1, want_refr);
+        if (dense) *spawned = (want_refl ? 1 : 0) | (want_refr ? 2 : 0);
         if (B.stats) {  // pruned zero-weight rays (statistics frames only)
             wave_count(line + 16, reflect_applies && !want_refl);
             wave_count(line + 16, refract_applies && !want_refr);
         }
         if (want_refl) {
-            if ((int64_t)at_refl < B.next_segcap) {
+            if (dense || (int64_t)at_refl < B.next_segcap) {
                 QueuedRay qo;
                 for (int k = 0; k < 3; ++k) {
                     qo.o[k] = c.over_point[k];
@@ -422,13 +426,13 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
                 qo.key = base | ((code * 2) & 0xFFFull);
                 qo.parent = (int32_t)node;
                 qo.slot = 0;
-                next_q[seg_base + (int64_t)at_refl] = qo;
+                next_q[dense ? node : seg_base + (int64_t)at_refl] = qo;
             } else {
                 atomicOr(err, kErrQueueOverflow);
             }
         }
         if (want_refr) {
-            if ((int64_t)at_refr < B.next_segcap) {
+            if (dense || (int64_t)at_refr < B.next_segcap) {
                 QueuedRay qo;
                 for (int k = 0; k < 3; ++k) {
                     qo.o[k] = c.under_point[k];
@@ -437,7 +441,7 @@ __device__ __forceinline__ bool prepare_node(const DevScene& S, const Batch& B, 
                 qo.key = base | ((code * 2 + 1) & 0xFFFull);
                 qo.parent = (int32_t)node;
                 qo.slot = 1;
-                next_q[seg_base + (int64_t)at_refr] = qo;
+                next_q[dense ? n + node : seg_base + (int64_t)at_refr] = qo;
             } else {
                 atomicOr(err, kErrQueueOverflow);
             }
@@ -501,7 +505,7 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const
           const double* __restrict__ hn12,
           NodeCols rec, ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q, unsigned long long* counters,
           unsigned* err, float* __restrict__ tbox, int tile_log2, float* __restrict__ stbox, int sub_log2,
-          int32_t* __restrict__ counts) {
+          int32_t* __restrict__ counts, uint8_t* __restrict__ spawn_flags) {
     const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double op[3] = {0.0, 0.0, 0.0};
     bool hit = false;
@@ -509,7 +513,16 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const
     // memset launch per level)
     if (node < n && counts != nullptr)
         for (int l = 0; l < S.num_lights; ++l) counts[node * S.num_lights + l] = 0;
-    if (node < n) hit = prepare_node<kPat>(S, B, q, n, hits, hn12, rec, heads, next_q, counters, err, node, op);
+    // (spawn_flags: the next level's queue dense, slot node / n + node taken where flag node / n + node is 1;
+    // every node writes both of its flags, so the array needs no clearing)
+    int spawned = 0;
+    if (node < n)
+        hit = prepare_node<kPat>(S, B, q, n, hits, hn12, rec, heads, next_q, counters, err, node, op,
+                                 spawn_flags != nullptr ? &spawned : nullptr);
+    if (node < n && spawn_flags != nullptr) {
+        spawn_flags[node] = (uint8_t)(spawned & 1);
+        spawn_flags[n + node] = (uint8_t)(spawned >> 1);
+    }
     if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2, stbox, sub_log2);
 }
 
@@ -2072,10 +2085,12 @@ struct frt_scene_handle {
     int64_t lit_flat_cap = 0;
     frt::LitStage* lit_stage = nullptr;  // (k_lit_stage's records, FRT_SHADE_STAGE)
     int64_t lit_stage_cap = 0;
-    int queue_sort = 1;                 // a level's queue read in parent order (FRT_QUEUE_SORT=0: the segments' order)
+    int queue_sort = 2;                 // a level's queue in parent order (FRT_QUEUE_SORT: 2 dense, 1 sorted, 0 off)
     int queue_sort_shift = 0;           // (FRT_QUEUE_SORT_SHIFT)
     uint32_t* qsort = nullptr;          // (its keys, their alternate buffer and the storage slots, 3 words per entry)
     int64_t qsort_cap = 0;
+    uint8_t* spawn_flags = nullptr;     // (FRT_QUEUE_SORT=2: the next level's taken slots, 2 per node)
+    int64_t spawn_flags_cap = 0;
     unsigned char* scan_tmp = nullptr;  // (the device sort's temporary storage)
     int64_t scan_tmp_cap = 0;
     unsigned* shade_lcount = nullptr;
@@ -3175,11 +3190,13 @@ int frt_scene_upload(const frt_scene* sc, int device, frt_scene_handle** out) {
         // round 5 did. Shipped frame: shade 14.2 / 13.1 / 12.9 ms for 0 / 1 / 2 (profiles/r06_ab_shipped_modes.txt)
         const char* se = std::getenv("FRT_SHADE_STAGE");
         h->shade_stage = h->sort_light >= 0 ? (se ? std::atoi(se) : 2) : 0;
-        // the secondary levels' queues read in parent order (reflected children, then refracted): a k_prepare
-        // block appends to segment blockIdx % kQueueSegs, so the segments' order puts children of pixels 256 apart
-        // side by side, and the shadow pass's tiles of consecutive nodes spread over the scene
+        // the secondary levels' queues read in parent order (reflected children, then refracted): appended to
+        // segment blockIdx % kQueueSegs, the segments' order put children of pixels 256 apart side by side, and the
+        // shadow pass's tiles of consecutive nodes spread over the scene. FRT_QUEUE_SORT: 2 (default) the children
+        // at fixed slots (no queue atomics) compacted in order; 1 the segments' entries radix-sorted by parent;
+        // 0 the segments' order (A/B runs, profiles/r06_ab_queue_sort.txt)
         const char* qs = std::getenv("FRT_QUEUE_SORT");
-        h->queue_sort = qs ? std::atoi(qs) : 1;
+        h->queue_sort = qs ? std::atoi(qs) : 2;
         const char* qsh = std::getenv("FRT_QUEUE_SORT_SHIFT");  // (A/B runs: parents' low bits out of the key)
         h->queue_sort_shift = qsh ? std::max(0, std::min(16, std::atoi(qsh))) : 0;
     }
@@ -3335,6 +3352,7 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->lit_row));
     hip_ignore(hipFree(h->lit_flat));
     hip_ignore(hipFree(h->qsort));
+    hip_ignore(hipFree(h->spawn_flags));
     hip_ignore(hipFree(h->lit_stage));
     hip_ignore(hipFree(h->scan_tmp));
     hip_ignore(hipFree(h->mixed));
@@ -4748,6 +4766,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             if (!h->S.cfg.all_ni_one && grow(&h->hn12, h->hn12_cap, 2 * n)) return -1;
             double* hn12 = h->S.cfg.all_ni_one ? nullptr : h->hn12;
             const QueuedRay* q = d == 0 ? nullptr : L.q;
+            bool dense = false;
             {
                 KTimer t(h, st, d == 0 ? 5 : 0);
                 launch_trace(h, B, q, n, h->hits, 0, hn12, true);
@@ -4765,11 +4784,26 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 int stl = 0;
                 while (subtiles && (1 << stl) < h->subtile) ++stl;
                 if (subtiles && grow(&h->stbox, h->stbox_cap, 6 * ((n >> stl) + 1))) return -1;
+                // the next level dense (FRT_QUEUE_SORT=2, default): child (node, slot) at slot n + node of its queue,
+                // the taken slots compacted in order (reflected children in parent order, then the refracted) into
+                // the next level's qperm, their count into counter word 20 (read back with the queue counts)
+                dense = h->queue_sort == 2 && d < path && 2 * n <= (int64_t)UINT32_MAX && N.cap >= 2 * n;
+                if (dense && (grow(&h->spawn_flags, h->spawn_flags_cap, 2 * n) || grow(&N.qperm, N.qperm_cap, 2 * n)))
+                    return -1;
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
                                    dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits, hn12,
                                    L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl,
-                                   subtiles ? h->stbox : nullptr, stl, L.counts);
+                                   subtiles ? h->stbox : nullptr, stl, L.counts, dense ? h->spawn_flags : nullptr);
                 FRT_HIP(hipGetLastError());
+                if (dense) {
+                    hipcub::CountingInputIterator<uint32_t> pos(0u);
+                    size_t tmp_bytes = 0;
+                    FRT_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_bytes, pos, h->spawn_flags, N.qperm,
+                                                          h->counters + 20, (int)(2 * n), h->stream));
+                    if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
+                    FRT_HIP(hipcub::DeviceSelect::Flagged((void*)h->scan_tmp, tmp_bytes, pos, h->spawn_flags, N.qperm,
+                                                          h->counters + 20, (int)(2 * n), h->stream));
+                }
             }
             // the next level's queue counts are final here (k_prepare appends the level's rays): their copy rides on
             // the shadow pass's first synchronize, and the level ends without one of its own
@@ -4884,7 +4918,7 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             // the next level's queue segments: prefix counts (a segment past its capacity is an error)
             int64_t next = 0;
             bool overflow = false;
-            for (int j = 0; j < kQueueSegs; ++j) {
+            for (int j = 0; j < kQueueSegs && !dense; ++j) {
                 N.hprefix[j] = next;
                 int64_t c = (int64_t)host_counters[(size_t)j * kCounterLine + d + 1];
                 if (c > B.next_segcap) {
@@ -4893,12 +4927,13 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 }
                 next += c;
             }
+            if (dense) next = (int64_t)host_counters[20];  // (the compaction's count)
             N.hprefix[kQueueSegs] = next;
             if (overflow) {
                 unsigned e = kErrQueueOverflow;
                 FRT_HIP(hipMemcpyAsync(h->err, &e, sizeof(unsigned), hipMemcpyHostToDevice, h->stream));
             }
-            if (next > 0 && d < path)
+            if (next > 0 && d < path && !dense)
                 FRT_HIP(hipMemcpyAsync(N.qprefix, N.hprefix.data(), (kQueueSegs + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
                                        h->stream));
             count[d + 1] = d < path ? next : 0;
@@ -4906,9 +4941,9 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
             // parents' pixels; keys: refracted bit above the parent index
             int pbits = 1;
             while (pbits < 32 && (1ll << pbits) < n) ++pbits;
-            N.sorted = h->queue_sort != 0 && d < path && next >= 4096 && !overflow && pbits < 32 &&
-                       N.cap <= (int64_t)UINT32_MAX;
-            if (N.sorted) {
+            N.sorted = dense || (h->queue_sort == 1 && d < path && next >= 4096 && !overflow && pbits < 32 &&
+                                 N.cap <= (int64_t)UINT32_MAX);
+            if (N.sorted && !dense) {
                 KTimer t(h, st, 6);
                 if (grow(&h->qsort, h->qsort_cap, 3 * next) || grow(&N.qperm, N.qperm_cap, next)) return -1;
                 uint32_t *keys = h->qsort, *keys2 = h->qsort + next, *slots = h->qsort + 2 * next;

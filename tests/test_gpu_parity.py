@@ -538,3 +538,19 @@ def test_render_multi_canvas_is_pinned_and_pooled(built):
     z = render_multi(sc, devices="0")
     assert z.ctypes.data == px and np.array_equal(z, y)
     release_render_multi()
+
+
+@pytest.mark.parametrize("name,rows", [("reflect_refract_test_150", None), ("cornell_direct_64_4x4", None),
+                                       ("cornell_gi_24", None), ("cornell_shipped_48_4x4", None),
+                                       ("cornell_direct_1920x1080_8x8", (300, 308))])
+def test_queue_order_equals_segment_order(built, name, rows):
+    """The secondary levels' nodes in parent order (FRT_QUEUE_SORT): 2 (default) children at fixed slots n * slot +
+    node compacted in order, 1 the segmented queue radix-sorted by (slot, parent), 0 the segments' append order.
+    Node order decides only which nodes share a wave or a beam tile, never what a node computes (keys carry the
+    sample and heap code, the combine writes through parent and slot), so the canvases are equal bit for bit:
+    reflection and refraction, a GI scene, the multi-row light and a band of the headline frame."""
+    kw = {} if rows is None else {"row_begin": rows[0], "row_end": rows[1]}
+    ref = _render_env(name, {"FRT_QUEUE_SORT": "0"}, **kw)
+    assert np.isfinite(ref).all() and ref[:, :, :3].max() > 0
+    for mode in ("1", "2"):
+        assert np.array_equal(_render_env(name, {"FRT_QUEUE_SORT": mode}, **kw), ref), mode
