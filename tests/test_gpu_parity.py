@@ -542,7 +542,7 @@ def test_render_multi_canvas_is_pinned_and_pooled(built):
 
 @pytest.mark.parametrize("name,rows", [("reflect_refract_test_150", None), ("cornell_direct_64_4x4", None),
                                        ("cornell_gi_24", None), ("cornell_shipped_48_4x4", None),
-                                       ("cornell_direct_1920x1080_8x8", (300, 308))])
+                                       ("cornell_direct_1920x1080_8x8", (700, 708))])
 def test_queue_order_equals_segment_order(built, name, rows):
     """The secondary levels' nodes in parent order (FRT_QUEUE_SORT): 2 (default) children at fixed slots n * slot +
     node compacted in order, 1 the segmented queue radix-sorted by (slot, parent), 0 the segments' append order.
