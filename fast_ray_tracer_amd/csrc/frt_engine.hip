@@ -505,7 +505,7 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const
           const double* __restrict__ hn12,
           NodeCols rec, ShadowHead* __restrict__ heads, QueuedRay* __restrict__ next_q, unsigned long long* counters,
           unsigned* err, float* __restrict__ tbox, int tile_log2, float* __restrict__ stbox, int sub_log2,
-          int32_t* __restrict__ counts, uint8_t* __restrict__ spawn_flags) {
+          int32_t* __restrict__ counts, unsigned long long* __restrict__ spawn_masks) {
     const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double op[3] = {0.0, 0.0, 0.0};
     bool hit = false;
@@ -513,15 +513,19 @@ k_prepare(DevScene S, Batch B, const QueuedRay* __restrict__ q, int64_t n, const
     // memset launch per level)
     if (node < n && counts != nullptr)
         for (int l = 0; l < S.num_lights; ++l) counts[node * S.num_lights + l] = 0;
-    // (spawn_flags: the next level's queue dense, slot node / n + node taken where flag node / n + node is 1;
-    // every node writes both of its flags, so the array needs no clearing)
+    // (spawn_masks: the next level's queue dense, slot node / n + node taken; per wave of 64 nodes g the lanes'
+    // reflected / refracted bits as masks g / G + g, G = the level's waves; every wave writes both, no clearing)
     int spawned = 0;
     if (node < n)
         hit = prepare_node<kPat>(S, B, q, n, hits, hn12, rec, heads, next_q, counters, err, node, op,
-                                 spawn_flags != nullptr ? &spawned : nullptr);
-    if (node < n && spawn_flags != nullptr) {
-        spawn_flags[node] = (uint8_t)(spawned & 1);
-        spawn_flags[n + node] = (uint8_t)(spawned >> 1);
+                                 spawn_masks != nullptr ? &spawned : nullptr);
+    if (spawn_masks != nullptr) {  // (every lane of the wave is here)
+        const unsigned long long mr = __ballot(spawned & 1), mt = __ballot((spawned >> 1) & 1);
+        const int64_t g = node >> 6, G = (n + 63) >> 6;
+        if ((threadIdx.x & 63) == 0 && g < G) {
+            spawn_masks[g] = mr;
+            spawn_masks[G + g] = mt;
+        }
     }
     if (tbox != nullptr) tile_box(node, n, hit, op, tbox, tile_log2, stbox, sub_log2);
 }
@@ -994,6 +998,30 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, Batch B, NodeCols 
 // A secondary level's queue entries with their parent-order keys (the reflected children first, then the
 // refracted, each in parent order) and storage slots, for the radix sort behind Batch.qperm (FRT_QUEUE_SORT).
 // B: the level's queue segments (qprefix, qsegcap).
+// FRT_QUEUE_SORT=2: the taken slots of the dense queue in order, from k_prepare's masks (2G of them) and the
+// exclusive scan of their popcounts (offs, 2G + 1 entries: offs[2G] the total, into counter word 20). One thread
+// per mask: slot = (g < G ? 0 : n) + 64 (g mod G) + bit.
+struct MaskPopc {
+    const unsigned long long* m;
+    int64_t count;
+    __host__ __device__ uint32_t operator()(int64_t i) const { return i < count ? (uint32_t)__popcll(m[i]) : 0u; }
+};
+__global__ void __launch_bounds__(kBlock) k_spawn_expand(const unsigned long long* __restrict__ masks,
+                                                         const uint32_t* __restrict__ offs, int64_t n, int64_t G,
+                                                         uint32_t* __restrict__ qperm,
+                                                         unsigned long long* __restrict__ counters) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g == 0) counters[20] = offs[2 * G];
+    if (g >= 2 * G) return;
+    unsigned long long m = masks[g];
+    uint32_t at = offs[g];
+    const uint32_t slot0 = (uint32_t)((g < G ? 0 : n) + ((g < G ? g : g - G) << 6));
+    while (m != 0ull) {
+        qperm[at++] = slot0 + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1ull;
+    }
+}
+
 // (shift: the parents' low bits left out of the key, runs of 2^shift parents in the segments' order)
 __global__ void __launch_bounds__(kBlock) k_queue_keys(Batch B, const QueuedRay* __restrict__ q, int64_t n, int pbits,
                                                        int shift, uint32_t* __restrict__ keys,
@@ -2089,8 +2117,10 @@ struct frt_scene_handle {
     int queue_sort_shift = 0;           // (FRT_QUEUE_SORT_SHIFT)
     uint32_t* qsort = nullptr;          // (its keys, their alternate buffer and the storage slots, 3 words per entry)
     int64_t qsort_cap = 0;
-    uint8_t* spawn_flags = nullptr;     // (FRT_QUEUE_SORT=2: the next level's taken slots, 2 per node)
-    int64_t spawn_flags_cap = 0;
+    unsigned long long* spawn_masks = nullptr;  // (FRT_QUEUE_SORT=2: the next level's taken slots, k_prepare)
+    int64_t spawn_masks_cap = 0;
+    uint32_t* spawn_offs = nullptr;              // (their popcounts' exclusive scan)
+    int64_t spawn_offs_cap = 0;
     unsigned char* scan_tmp = nullptr;  // (the device sort's temporary storage)
     int64_t scan_tmp_cap = 0;
     unsigned* shade_lcount = nullptr;
@@ -3352,7 +3382,8 @@ void frt_scene_release(frt_scene_handle* h) {
     hip_ignore(hipFree(h->lit_row));
     hip_ignore(hipFree(h->lit_flat));
     hip_ignore(hipFree(h->qsort));
-    hip_ignore(hipFree(h->spawn_flags));
+    hip_ignore(hipFree(h->spawn_masks));
+    hip_ignore(hipFree(h->spawn_offs));
     hip_ignore(hipFree(h->lit_stage));
     hip_ignore(hipFree(h->scan_tmp));
     hip_ignore(hipFree(h->mixed));
@@ -4788,21 +4819,28 @@ static int render_frame(frt_scene_handle* h, const frt_frame_params* P, double* 
                 // the taken slots compacted in order (reflected children in parent order, then the refracted) into
                 // the next level's qperm, their count into counter word 20 (read back with the queue counts)
                 dense = h->queue_sort == 2 && d < path && 2 * n <= (int64_t)UINT32_MAX && N.cap >= 2 * n;
-                if (dense && (grow(&h->spawn_flags, h->spawn_flags_cap, 2 * n) || grow(&N.qperm, N.qperm_cap, 2 * n)))
+                const int64_t G = (n + 63) >> 6;
+                if (dense && (grow(&h->spawn_masks, h->spawn_masks_cap, 2 * G) ||
+                              grow(&h->spawn_offs, h->spawn_offs_cap, 2 * G + 1) || grow(&N.qperm, N.qperm_cap, 2 * n)))
                     return -1;
                 hipLaunchKernelGGL(h->S.num_patterns > 0 ? k_prepare<true> : k_prepare<false>, dim3(grid_for(n)),
                                    dim3(kBlock), 0, h->stream, h->S, B, q, n, h->hits, hn12,
                                    L.rec, L.head, N.q, h->counters, h->err, tiles ? h->tbox : nullptr, tl,
-                                   subtiles ? h->stbox : nullptr, stl, L.counts, dense ? h->spawn_flags : nullptr);
+                                   subtiles ? h->stbox : nullptr, stl, L.counts, dense ? h->spawn_masks : nullptr);
                 FRT_HIP(hipGetLastError());
                 if (dense) {
-                    hipcub::CountingInputIterator<uint32_t> pos(0u);
+                    hipcub::CountingInputIterator<int64_t> idx(0);
+                    hipcub::TransformInputIterator<uint32_t, MaskPopc, hipcub::CountingInputIterator<int64_t>> popc(
+                        idx, MaskPopc{h->spawn_masks, 2 * G});
                     size_t tmp_bytes = 0;
-                    FRT_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_bytes, pos, h->spawn_flags, N.qperm,
-                                                          h->counters + 20, (int)(2 * n), h->stream));
+                    FRT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, popc, h->spawn_offs, (int)(2 * G + 1),
+                                                             h->stream));
                     if (grow(&h->scan_tmp, h->scan_tmp_cap, (int64_t)tmp_bytes + 16)) return -1;
-                    FRT_HIP(hipcub::DeviceSelect::Flagged((void*)h->scan_tmp, tmp_bytes, pos, h->spawn_flags, N.qperm,
-                                                          h->counters + 20, (int)(2 * n), h->stream));
+                    FRT_HIP(hipcub::DeviceScan::ExclusiveSum((void*)h->scan_tmp, tmp_bytes, popc, h->spawn_offs,
+                                                             (int)(2 * G + 1), h->stream));
+                    hipLaunchKernelGGL(k_spawn_expand, dim3(grid_for(2 * G)), dim3(kBlock), 0, h->stream, h->spawn_masks,
+                                       h->spawn_offs, n, G, N.qperm, h->counters);
+                    FRT_HIP(hipGetLastError());
                 }
             }
             // the next level's queue counts are final here (k_prepare appends the level's rays): their copy rides on
