@@ -720,16 +720,13 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                                 edh = fmax(0.0, dot3(nr.eyev, hv));
                                 ldh = dot3(lv, hv);
                             }
-                            const double edh_inv = recip_shade(edh);
                             double dist_term = kFactored ? pow_apply(ndh, nsd, pplan) * cdist
                                                          : (nr.Ns + 2) * pow_ns(ndh, nr.Ns) * 0.5 * k1Pi;
-                            double gc = 2.0 * ndh * edh_inv;
-                            double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
                             // pow(1 - ldh, 5.0) (renderer.c:969) by squaring: within an ulp or two of the
                             // reference's libm pow, like the device pow it replaces
                             const double om = 1.0 - ldh, om2 = om * om;
                             double factor = om2 * om2 * om;
-                            double brdf = div_shade(dist_term * geo, 4.0 * ndl * ned);
+                            double brdf = brdf_shade(dist_term, ndh, edh, ndl, ned);
                             if (kFactored) {
                                 sum_b += brdf;
                                 sum_fb += factor * brdf;
@@ -755,13 +752,10 @@ __device__ __forceinline__ void shade_node(const DevScene& S, const Batch& B, co
                     constexpr bool kPair = FRT_SHADE_PAIR && kAlg && kFactored && FRT_SHADE_FAST;
                     // the specular terms of one point past its tail test (term()'s arithmetic)
                     auto spec_rest = [&](double ndl, double ndh, double edh, double ldh) {
-                        const double edh_inv = recip_shade(edh);
                         const double dist_term = pow_apply(ndh, nsd, pplan) * cdist;
-                        const double gc = 2.0 * ndh * edh_inv;
-                        const double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
                         const double om = 1.0 - ldh, om2 = om * om;
                         const double factor = om2 * om2 * om;
-                        const double brdf = div_shade(dist_term * geo, 4.0 * ndl * ned);
+                        const double brdf = brdf_shade(dist_term, ndh, edh, ndl, ned);
                         sum_b += brdf;
                         sum_fb += factor * brdf;
                     };
@@ -2756,6 +2750,13 @@ __global__ void k_math_selftest(int64_t n, uint64_t seed, unsigned long long* ba
         b += !(fabs(frt::recip_shade(s) - inv) <= 0x1p-46 * inv);
         const double a = fabs(v[0]) >= 0x1p-600 ? fabs(v[0]) : 0.0;
         b += !(fabs(frt::div_shade(a, s) - a / s) <= 0x1p-46 * (a / s));
+        // the BRDF factor with one reciprocal (brdf_shade) within 2^-44 relative of the reference's two quotients
+        // (renderer.c:952-963), dot products from the unit vector's components
+        const double nh = fabs(r[0]), eh = fabs(r[1]), nl = fabs(r[2]), ne = fmax(fabs(r[0] * r[1]), 0x1p-20);
+        const double gc = 2.0 * nh * (1.0 / eh);
+        const double ref = (a * fmin(1.0, fmin(gc * ne, gc * nl))) / (4.0 * nl * ne);
+        const double got = frt::brdf_shade(a, nh, eh, nl, ne);
+        if (__builtin_isfinite(ref)) b += !(got == ref || fabs(got - ref) <= 0x1p-44 * fabs(ref));
     }
     if (b) atomicAdd(bad, b);
 }

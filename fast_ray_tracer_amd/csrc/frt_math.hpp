@@ -156,6 +156,33 @@ __device__ __forceinline__ double div_shade(double a, double b) {
     }
     return q;
 }
+// lighting_microfacet's brdf_factor (renderer.c:952-963): D G / (4 (n.l)(n.e)), G = min(1, gc (n.e), gc (n.l)),
+// gc = 2 (n.h) / (e.h). FRT_SHADE_MERGE (default 1) takes one reciprocal where the reference divides twice: the
+// three candidates of G scaled by e.h > 0 keep their order, so G (e.h) = min(e.h, 2 (n.h)(n.e), 2 (n.h)(n.l)) and
+// brdf = D min(..) / ((e.h) 4 (n.l)(n.e)) — a few ulps from the two-quotient form, like the estimates above. A lane
+// whose operands leave [2^-600, 2^600] (e.h = 0 among them: the reference's 1 / (e.h) is inf there and G = 1)
+// takes the reference's form with IEEE quotients. (FRT_SHADE_MERGE=0 builds: a reciprocal and a quotient, A/B runs)
+#ifndef FRT_SHADE_MERGE
+#define FRT_SHADE_MERGE 1
+#endif
+__device__ __forceinline__ double brdf_shade(double D, double ndh, double edh, double ndl, double ned) {
+    if (FRT_SHADE_MERGE && FRT_SHADE_FAST) {
+        const double g2 = 2.0 * ndh;
+        const double a = D * fmin(edh, fmin(g2 * ned, g2 * ndl)), b = edh * (4.0 * ndl * ned);
+        double q = a * rcp_nr(b);
+        const bool slow = !(shade_in_range(edh) && shade_in_range(b) && (a == 0.0 || shade_in_range(a)));
+        if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+            if (slow) {
+                const double gc = 2.0 * ndh * (1.0 / edh);
+                q = (D * fmin(1.0, fmin(gc * ned, gc * ndl))) / (4.0 * ndl * ned);
+            }
+        }
+        return q;
+    }
+    const double gc = 2.0 * ndh * recip_shade(edh);
+    const double geo = fmin(1.0, fmin(gc * ned, gc * ndl));
+    return div_shade(D * geo, 4.0 * ndl * ned);
+}
 
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* r) {
     double x = a[1] * b[2] - a[2] * b[1];
