@@ -321,6 +321,30 @@ __device__ __forceinline__ double photon_d2(const PhotonMapDev& M, int32_t p, co
     return v;
 }
 
+// The sum passes' record prefetch (FRT_SUM_TOUCH=1 builds, A/B runs; off by default: k_gather_est 1266 -> 1285 ms
+// per cornell_gi_480x270_8x8 frame with it, profiles/r06_ab_gi_touch.txt): the sum over a query's nearest photons
+// reads one 64-lane chunk of 80-byte records per round trip (a second chunk in flight costs 20 VGPRs and spills),
+// and the sum was 55.6 % of the estimate's cycles (profiles/r06_gi_est_phases.txt). While a chunk is summed, each
+// lane loads one word from each 64-byte line of its record in the next chunk (two VGPRs), so that chunk's record
+// loads would find their lines in the CU's vector L1; the touched words are folded together and read by an empty
+// asm statement after the loop (sum_touch_keep). The records are L1 / L2 hits already: the round trips it hides
+// cost less than its loads and the wait its loop-carried registers force at the end of every chunk.
+#ifndef FRT_SUM_TOUCH
+#define FRT_SUM_TOUCH 0
+#endif
+struct SumTouch {
+    uint32_t a = 0, b = 0, keep = 0;
+    // (every lane loads: a lane past the list's end touches its last entry, so no branch splits the loop body)
+    __device__ __forceinline__ void next(const PhotonMapDev& M, int32_t p) {
+        keep ^= a ^ b;  // (the previous chunk's words: loaded a whole chunk ago)
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(M.rec + 10 * (int64_t)p);
+        a = q[0];
+        b = q[19];
+    }
+};
+// (an empty asm statement reads the folded words: the loads stay live, no instruction is emitted)
+__device__ __forceinline__ void sum_touch_keep(uint32_t t) { asm volatile("" ::"v"(t)); }
+
 __device__ __forceinline__ int32_t photon_heap(const PhotonMapDev& M, int32_t p) {
     return (int32_t)__double_as_longlong(M.rec[10 * (int64_t)p + 9]);
 }
@@ -620,6 +644,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     };
     if (total <= (unsigned)k) {  // every photon in range: no heap, dist2[0] = max_dist^2
         if (listed) {  // kSumChunks chunks of the list per round trip
+            SumTouch tch;  // (FRT_SUM_TOUCH)
             for (unsigned base = 0; base < count; base += 64u * kSumChunks) {
                 PhotonRec rc[kSumChunks];
                 bool ok[kSumChunks];
@@ -632,10 +657,12 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                     EST_LANES(15, ok[c]);
                     if (ok[c]) rc[c] = photon_rec(M, pc[c]);
                 }
+                if (FRT_SUM_TOUCH) tch.next(M, (int32_t)L.ent[min(base + 64u * kSumChunks + (unsigned)lane, count - 1u)].y);
 #pragma unroll
                 for (int c = 0; c < kSumChunks; ++c)
                     if (ok[c]) accumulate(rc[c], pc[c], sqrt_w(rc[c].d2(x)));
             }
+            if (FRT_SUM_TOUCH) sum_touch_keep(tch.keep ^ tch.a ^ tch.b);
         } else {
             visit([&](int32_t p, bool in, unsigned) {
                 EST_LANES(15, in);
@@ -779,6 +806,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
     // loads issue with near_mask's
     const unsigned qmask = near_mask(M.kd, R, x);
     if (compact) {
+        SumTouch tch;  // (FRT_SUM_TOUCH)
         for (unsigned base = 0; base < c_in; base += 64u * kSumChunks) {
             PhotonRec rc[kSumChunks];
             bool ok[kSumChunks];
@@ -791,6 +819,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                 EST_LANES(15, ok[c]);
                 if (ok[c]) rc[c] = photon_rec(M, pc[c]);
             }
+            if (FRT_SUM_TOUCH) tch.next(M, (int32_t)L.sel[min(base + 64u * kSumChunks + (unsigned)lane, c_in - 1u)]);
 #pragma unroll
             for (int c = 0; c < kSumChunks; ++c)
                 if (ok[c]) {
@@ -798,6 +827,7 @@ __device__ __forceinline__ int64_t wave_irradiance_estimate(const PhotonMapDev& 
                     before_all = before_all && found_before(rc[c].heap(), R, qmask);
                 }
         }
+        if (FRT_SUM_TOUCH) sum_touch_keep(tch.keep ^ tch.a ^ tch.b);
     }
     if (!compact || !fast) visit([&](int32_t p, bool in, unsigned key) {
         const bool certain = in && key < blo && !compact;
