@@ -3531,9 +3531,9 @@ static void launch_trace_redo_f(frt_scene_handle* h, const frt::Batch& B, const 
                        hits, h->err, h->tredo, (const unsigned*)(h->tredo + cap), cap);
 }
 
-// hn12: where the hits' refractive indices go (null: every index is one, or nobody reads them); jit: the path's
-// own rays (camera rays and their reflections: the scene-specialised closest hit where the scene has one; the
-// final gather's incoherent hemisphere rays measured faster on the generic walk, profiles/r04_ab_gi_trace.txt)
+// hn12: where the hits' refractive indices go (null: every index is one, or nobody reads them); jit: the
+// scene-specialised closest hit where the scene has one (the path's own rays, and since round 6 the final gather's
+// hemisphere rays: profiles/r06_ab_gather_jit.txt)
 static void launch_trace(frt_scene_handle* h, const frt::Batch& B, const frt::QueuedRay* q, int64_t n,
                          frt::HitRec* hits = nullptr, int filter_casts = 0, double* hn12 = nullptr, bool jit = false) {
     if (hits == nullptr) hits = h->hits;
@@ -4581,7 +4581,11 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
             frt::Batch Bg = B;  // the gather rays form one contiguous queue
             Bg.qprefix = nullptr;
             Bg.qperm = nullptr;
-            launch_trace(h, Bg, G.gq, rays, G.ghits, 0);
+            // the hemisphere rays through the scene-specialised closest hit where the scene has one (1387 -> 1363 ms per
+            // cornell_gi_480x270_8x8 frame, profiles/r06_ab_gather_jit.txt; round 4's slower kernel lost there,
+            // profiles/r04_ab_gi_trace.txt); FRT_GATHER_JIT=0: the generic walk (A/B runs)
+            static const bool gather_jit = !(std::getenv("FRT_GATHER_JIT") && std::atoi(std::getenv("FRT_GATHER_JIT")) == 0);
+            launch_trace(h, Bg, G.gq, rays, G.ghits, 0, nullptr, gather_jit);
             // FRT_GATHER_QUEUE=0: the static request ranges (A/B runs)
             const char* qenv = std::getenv("FRT_GATHER_QUEUE");
             const bool queue = !(qenv && std::strcmp(qenv, "0") == 0) && rays < (int64_t)0xF0000000u;
