@@ -1,0 +1,6 @@
+#!/bin/bash
+# round 6 final evidence on the final device sources (a): kernel stats + PMC passes of the headline and cfg3 (tools/prof.sh)
+set -o pipefail
+bash tools/prof.sh r06z_headline cornell_direct_1920x1080_8x8 \
+    "k_shade_lit k_prepare frt_jit_sub frt_jit_shadow frt_jit_trace frt_jit_subtile frt_jit_tile k_combine_resolve" || exit 1
+bash tools/prof.sh r06z_cfg3 cornell_direct_800_4x4 "k_shade_lit k_prepare frt_jit_sub frt_jit_shadow frt_jit_trace frt_jit_subtile frt_jit_tile" || exit 1
