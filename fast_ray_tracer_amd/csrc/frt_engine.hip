@@ -4584,14 +4584,15 @@ static int shade_gi(frt_scene_handle* h, const frt::Batch& B, frt_scene_handle::
             // the hemisphere rays through the scene-specialised closest hit where the scene has one (1387 -> 1363 ms per
             // cornell_gi_480x270_8x8 frame, profiles/r06_ab_gather_jit.txt; round 4's slower kernel lost there,
             // profiles/r04_ab_gi_trace.txt); FRT_GATHER_JIT=0: the generic walk (A/B runs)
-            static const bool gather_jit = !(std::getenv("FRT_GATHER_JIT") && std::atoi(std::getenv("FRT_GATHER_JIT")) == 0);
+            // (read per chunk, like the knobs below: a test switches them between frames of one process)
+            const bool gather_jit = !(std::getenv("FRT_GATHER_JIT") && std::atoi(std::getenv("FRT_GATHER_JIT")) == 0);
             launch_trace(h, Bg, G.gq, rays, G.ghits, 0, nullptr, gather_jit);
             // FRT_GATHER_QUEUE=0: the static request ranges (A/B runs)
             const char* qenv = std::getenv("FRT_GATHER_QUEUE");
             const bool queue = !(qenv && std::strcmp(qenv, "0") == 0) && rays < (int64_t)0xF0000000u;
             // the requests in the spatial order of their points from 4096 of them (FRT_GATHER_SORT=0: gather order,
             // =1: sorted at any count)
-            static const int sort_mode = std::getenv("FRT_GATHER_SORT") ? std::atoi(std::getenv("FRT_GATHER_SORT")) : -1;
+            const int sort_mode = std::getenv("FRT_GATHER_SORT") ? std::atoi(std::getenv("FRT_GATHER_SORT")) : -1;
             const bool sorted = queue && sort_mode != 0 && (rays >= 4096 || sort_mode == 1) && rays < (int64_t)0x7FFFFFFF;
             if (sorted && grow(&G.gkeys, G.gkeys_cap, 4 * rays)) return -1;
             uint32_t *k0 = G.gkeys, *k1 = G.gkeys + rays, *i0 = G.gkeys + 2 * rays, *i1 = G.gkeys + 3 * rays;

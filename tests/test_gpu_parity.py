@@ -389,6 +389,16 @@ def test_gather_order_equals_request_order(built):
     assert np.array_equal(ordered, plain)
 
 
+def test_gather_rays_jit_equals_generic_walk(built):
+    """The final gather's hemisphere rays through the scene-specialised closest hit (frt_jit_trace with k_trace_redo
+    for the rays it cannot decide; the default since round 6) must give the GI canvas of the generic walk
+    (FRT_GATHER_JIT=0), bit for bit: the hit records are the same, only the kernel that finds them changes."""
+    jit = _render_frame_env("cornell_gi_24", {"FRT_GATHER_JIT": "1"})
+    plain = _render_frame_env("cornell_gi_24", {"FRT_GATHER_JIT": "0"})
+    assert np.isfinite(jit).all()
+    assert np.array_equal(jit, plain)
+
+
 @pytest.mark.parametrize("name", ["bounding_boxes_800x1000_4x4", "bounding_boxes_100x125_4x4", "teapot_low_100",
                                   "nave_120x150_4x4", "degenerate_mesh_48"])
 def test_mesh_search_equals_generic_walk(built, name):
